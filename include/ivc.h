@@ -1,0 +1,168 @@
+/*
+ * ivc.h — C-ABI of the MI355X-native ivclab block-codec core (libivc.so).
+ *
+ * The reference (n2oblife/ivclab) is pure Python/NumPy and has no FFI of its own; the
+ * drop-in boundary is its Python class API.  Every entry point below replaces the body of
+ * one reference method (cited per function); the Python host mirror in ivclab_amd/ keeps
+ * the reference signatures and calls these through ctypes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  No torch / numpy types in any signature.
+ *  - Return value: IVC_OK (0) on success, a negative IVC_E* code on failure; the message
+ *    for the calling thread is available from ivc_last_error().
+ *  - Functions WITHOUT the _dev suffix take HOST buffers (C-contiguous), stage them through
+ *    per-device scratch memory owned by the library, and return when the result is back in
+ *    the caller's host buffer (synchronous, like the NumPy reference).
+ *  - Functions WITH the _dev suffix take DEVICE pointers (caller-owned, e.g. torch tensors)
+ *    and a hipStream_t passed as void*; they only enqueue work (asynchronous).
+ *  - Element-type codes (ivc_dtype) name the NumPy dtype the reference would see; the
+ *    arithmetic follows NumPy's promotion rules for that dtype.
+ */
+#ifndef IVC_H
+#define IVC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* element types (NumPy dtype of the array handed to the reference method) */
+enum ivc_dtype {
+  IVC_U8 = 1, IVC_I8 = 2, IVC_U16 = 3, IVC_I16 = 4, IVC_U32 = 5, IVC_I32 = 6,
+  IVC_U64 = 7, IVC_I64 = 8, IVC_F32 = 9, IVC_F64 = 10
+};
+
+/* scipy.fft norm argument of DiscreteCosineTransform(norm=...) (ivclab/signal/dct.py:9-10) */
+enum ivc_norm { IVC_NORM_BACKWARD = 0, IVC_NORM_ORTHO = 1, IVC_NORM_FORWARD = 2 };
+
+/* motion-estimation SSD semantics */
+enum ivc_me_mode {
+  IVC_ME_NUMPY = 0,    /* NumPy semantics of the element type: modular integer sub/square,
+                          pairwise float sums (ivclab/video/motion.py:46)                  */
+  IVC_ME_EXACT_U8 = 1  /* u8 storage of integer-valued frames, SSD exact = the reference run
+                          on frame.astype(float64) (what VideoCodec passes, videocodec.py:38) */
+};
+
+enum ivc_status {
+  IVC_OK = 0, IVC_E_ARG = -1, IVC_E_DTYPE = -2, IVC_E_SHAPE = -3, IVC_E_DEVICE = -4,
+  IVC_E_NOMEM = -5
+};
+
+/* ---------------------------------------------------------------- runtime ---------- */
+const char* ivc_last_error(void);
+int ivc_version(void);
+int ivc_device_count(void);
+int ivc_set_device(int device);
+/* 1 if the loaded code object matches the current device (gfx950), 0 otherwise */
+int ivc_device_ok(void);
+/* release the library's cached scratch buffers on the current device */
+int ivc_release_scratch(void);
+
+/* ---------------------------------------------------------------- DCT -------------- */
+/* 2-D DCT-II (inverse=0) / DCT-III (inverse=1) of nblk contiguous 8x8 blocks, applied along
+ * the last axis then the second-to-last, exactly as scipy.fft.dct/idct (pocketfft) computes
+ * it.  dst_dtype must be IVC_F32 or IVC_F64 (scipy: float32 stays float32, every integer
+ * type and float64 compute in float64).
+ * Replaces: DiscreteCosineTransform.transform          ivclab/signal/dct.py:12-28
+ *           DiscreteCosineTransform.inverse_transform  ivclab/signal/dct.py:30-46        */
+int ivc_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
+               int inverse, int norm);
+int ivc_dct8x8_dev(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
+                   int inverse, int norm, void* stream);
+
+/* ---------------------------------------------------------------- quantization ----- */
+/* src: nblk x C x 64 (C = 1 or 3; C = 1 broadcasts over the 3 table planes), table: the
+ * 3 x 64 scaled quantization table as returned by get_quantization_table() (values exactly
+ * representable in calc_dtype), calc_dtype: NumPy result type of src / table (IVC_F32 or
+ * IVC_F64).  dst: nblk x 3 x 64 int32 = astype(int32)(round_half_even(src / table)).
+ * Replaces: PatchQuant.quantize    ivclab/quantization/patchquant.py:44-60              */
+int ivc_quantize(const void* src, int src_dtype, int64_t nblk, int C, const double* table,
+                 int calc_dtype, int32_t* dst);
+int ivc_quantize_dev(const void* src, int src_dtype, int64_t nblk, int C, const double* table,
+                     int calc_dtype, int32_t* dst, void* stream);
+
+/* dst = astype(int32)(src * table) computed in calc_dtype (truncation toward zero).
+ * Replaces: PatchQuant.dequantize  ivclab/quantization/patchquant.py:62-78              */
+int ivc_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const double* table,
+                   int calc_dtype, int32_t* dst);
+int ivc_dequantize_dev(const void* src, int src_dtype, int64_t nblk, int C,
+                       const double* table, int calc_dtype, int32_t* dst, void* stream);
+
+/* ---------------------------------------------------------------- zig-zag ---------- */
+/* nrow rows of 64 elements of elem_size bytes (1, 2, 4 or 8).  inverse=0: ZigZag.flatten
+ * (dst[order[k]] = src[k]); inverse=1: ZigZag.unflatten (dst[k] = src[order[k]]).
+ * src_row_stride (elements, >= 64) lets unflatten read rows wider than 64.
+ * Replaces: ZigZag.flatten / unflatten  ivclab/utils/shape.py:21-36,
+ *           zigzag_scan                 ivclab/signal/zigzag.py:3-26                    */
+int ivc_zigzag(const void* src, int64_t nrow, int64_t src_row_stride, int elem_size,
+               int inverse, void* dst);
+int ivc_zigzag_dev(const void* src, int64_t nrow, int64_t src_row_stride, int elem_size,
+                   int inverse, void* dst, void* stream);
+
+/* ---------------------------------------------------------------- fused intra ------ */
+/* patch -> DCT-II(ortho) -> quantize (-> zig-zag) over nframes images [H][W][C]
+ * (H, W multiples of 8, C = 1 or 3).  out: [nframes][H/8][W/8][3][64] int32 (raster or
+ * zig-zag order inside each 64).  Equals PatchQuant.quantize(DCT.transform(Patcher.patch(img)))
+ * (+ ZigZag.flatten) bit for bit.  table/calc_dtype as ivc_quantize (calc = result type of
+ * the DCT dtype and the table dtype).  hist (optional, may be NULL): int64[nbins] histogram
+ * of the emitted coefficients, bin = value - hist_lo, values outside [hist_lo,
+ * hist_lo+nbins) counted in the first/last bin; accumulated (not cleared) by the call.
+ * Replaces the hot part of IntraCodec.image2symbols  ivclab/image/intracodec.py:66-75     */
+int ivc_intra_encode(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W, int C,
+                     const double* table, int calc_dtype, int zigzag, int32_t* out);
+int ivc_intra_encode_dev(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
+                         int C, const double* table, int calc_dtype, int zigzag, int32_t* out,
+                         int64_t* hist, int32_t hist_lo, int32_t nbins, void* stream);
+
+/* (un-zig-zag ->) dequantize -> DCT-III(ortho) of nblk blocks of 3 x 64 int32 symbols.
+ * out: nblk x 3 x 8 x 8 float64 = DCT.inverse_transform(PatchQuant.dequantize(ZigZag.unflatten(q)))
+ * Replaces the hot part of IntraCodec.symbols2image  ivclab/image/intracodec.py:115-121   */
+int ivc_intra_decode(const int32_t* q, int64_t nblk, const double* table, int calc_dtype,
+                     int unzigzag, double* out);
+int ivc_intra_decode_dev(const int32_t* q, int64_t nblk, const double* table, int calc_dtype,
+                         int unzigzag, double* out, void* stream);
+
+/* ---------------------------------------------------------------- motion ----------- */
+/* Full-search block matching, 8x8 blocks, displacement +-sr, SSD, first strict minimum in
+ * raster order of (dy, dx).  ref/cur: nframes x H x W (frame f of cur is matched against
+ * frame f of ref; H, W multiples of 8).  mv: nframes x H/8 x W/8 int64 indices
+ * (dy+sr)*(2sr+1)+(dx+sr).  mode: ivc_me_mode (IVC_ME_EXACT_U8 requires dtype IVC_U8).
+ * Replaces: MotionCompensator.compute_motion_vector  ivclab/video/motion.py:8-58        */
+int ivc_motion_estimate(const void* ref, const void* cur, int dtype, int64_t nframes,
+                        int64_t H, int64_t W, int sr, int mode, int64_t* mv);
+int ivc_motion_estimate_dev(const void* ref, const void* cur, int dtype, int64_t nframes,
+                            int64_t H, int64_t W, int sr, int mode, int64_t* mv, void* stream);
+
+/* Block-copy motion compensation: out[y:y+8, x:x+8, :] = ref[y+dy:.., x+dx:.., :] for each
+ * block, zeros where the displaced block leaves the frame.  ref/out: nframes x H x W x C,
+ * elem_size bytes per element; mv as produced above.
+ * Replaces: MotionCompensator.reconstruct_with_motion_vector  ivclab/video/motion.py:60-97 */
+int ivc_motion_compensate(const void* ref, int elem_size, int64_t nframes, int64_t H,
+                          int64_t W, int64_t C, const int64_t* mv, int sr, void* out);
+int ivc_motion_compensate_dev(const void* ref, int elem_size, int64_t nframes, int64_t H,
+                              int64_t W, int64_t C, const int64_t* mv, int sr, void* out,
+                              void* stream);
+
+/* ---------------------------------------------------------------- fused inter ------ */
+/* Open-loop P-frame residual coding of a u8 luma sequence: for every
+ * frame f >= 1 of frames[nframes][H][W]: mv = ME(frames[f-1], frames[f]) (exact-u8 SSD),
+ * prediction = MC(frames[f-1], mv), residual = float64(frames[f]) - prediction,
+ * out = quantize(DCT(patch(residual))) as in ivc_intra_encode with C = 1.
+ * mv: (nframes-1) x H/8 x W/8 int64, out: (nframes-1) x H/8 x W/8 x 3 x 64 int32.
+ * Replaces VideoCodec.encode_decode's hot path  ivclab/video/videocodec.py:52-73         */
+int ivc_inter_encode_dev(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W, int sr,
+                         const double* table, int calc_dtype, int zigzag, int64_t* mv,
+                         int32_t* out, void* stream);
+
+/* ---------------------------------------------------------------- histogram -------- */
+/* hist[v - lo] += 1 for each symbol (values clamped into [lo, lo+nbins-1]); accumulates.
+ * Feeds the global Huffman table (ivclab/entropy/entropy.py:6-29 stats_marg).            */
+int ivc_histogram_i32(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, int64_t* hist);
+int ivc_histogram_i32_dev(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins,
+                          int64_t* hist, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IVC_H */

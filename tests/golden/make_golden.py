@@ -1,0 +1,201 @@
+"""Generate the golden input/output vectors for the hot path FROM THE REFERENCE ITSELF.
+
+Run in the build container (where /root/reference exists):
+    python tests/golden/make_golden.py
+It loads the reference hot-path modules by file path (the package __init__ needs the
+absent `constriction` wheel, so `import ivclab` itself fails; these modules import only
+numpy/scipy/einops), runs them on seeded synthetic inputs and writes small .npz fixtures
+next to this script.  Only data (inputs and the reference's outputs) is committed; nothing
+from the reference ships.  The GPU box never runs this script.
+
+Reference modules used (paths relative to /root/reference):
+  ivclab/signal/dct.py            DiscreteCosineTransform
+  ivclab/quantization/patchquant.py PatchQuant
+  ivclab/utils/shape.py           ZigZag, Patcher
+  ivclab/signal/zigzag.py         zigzag_scan
+  ivclab/video/motion.py          MotionCompensator
+"""
+import contextlib
+import importlib.util
+import io
+import os
+import sys
+
+import numpy as np
+
+REF = os.environ.get("IVC_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _load(rel, name):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, rel))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def _quiet(fn, *a):
+    with contextlib.redirect_stdout(io.StringIO()):
+        return fn(*a)
+
+
+def blocks_u8(rng, n):
+    """Mixed 8x8 uint8 content: noise, constants (DC ties), checkerboards, ramps."""
+    x = rng.integers(0, 256, (n, 8, 8)).astype(np.uint8)
+    k = n // 8
+    x[:k] = rng.integers(0, 256, (k, 1, 1))                                   # constant
+    cb = (np.indices((8, 8)).sum(0) % 2).astype(np.uint8)
+    x[k:2 * k] = cb[None] * rng.integers(0, 256, (k, 1, 1)).astype(np.uint8)  # checkerboard
+    ramp = np.add.outer(np.arange(8), np.arange(8))
+    x[2 * k:3 * k] = (ramp[None] * rng.integers(1, 17, (k, 1, 1))).clip(0, 255)  # ramps
+    x[3 * k] = 255
+    x[3 * k + 1] = 0
+    return x
+
+
+def image_u8(rng, H, W, C):
+    """Synthetic image built from the same block mix."""
+    b = blocks_u8(rng, (H // 8) * (W // 8) * C)
+    rng.shuffle(b)
+    return b.reshape(H // 8, W // 8, C, 8, 8).transpose(0, 3, 1, 4, 2).reshape(H, W, C).copy()
+
+
+def main():
+    dct_m = _load("ivclab/signal/dct.py", "ref_dct")
+    pq_m = _load("ivclab/quantization/patchquant.py", "ref_patchquant")
+    sh_m = _load("ivclab/utils/shape.py", "ref_shape")
+    zz_m = _load("ivclab/signal/zigzag.py", "ref_zigzag")
+    mo_m = _load("ivclab/video/motion.py", "ref_motion")
+    rng = np.random.default_rng(20250629)
+    DCT = dct_m.DiscreteCosineTransform()
+
+    # ---------------------------------------------------------------- DCT / IDCT
+    d = {}
+    d["x_u8"] = blocks_u8(rng, 1024)
+    d["dct_u8"] = DCT.transform(d["x_u8"])
+    d["x_f64"] = rng.normal(0, 60, (256, 8, 8))
+    d["dct_f64"] = DCT.transform(d["x_f64"])
+    d["idct_f64"] = DCT.inverse_transform(d["x_f64"])
+    d["x_f32"] = rng.normal(0, 60, (256, 8, 8)).astype(np.float32)
+    d["dct_f32"] = DCT.transform(d["x_f32"])
+    d["idct_f32"] = DCT.inverse_transform(d["x_f32"])
+    d["x_i32"] = rng.integers(-1200, 1200, (256, 8, 8)).astype(np.int32)
+    d["idct_i32"] = DCT.inverse_transform(d["x_i32"])
+    d["x_i16"] = rng.integers(-255, 256, (64, 8, 8)).astype(np.int16)
+    d["dct_i16"] = DCT.transform(d["x_i16"])
+    for norm in ("backward", "forward"):
+        D2 = dct_m.DiscreteCosineTransform(norm=norm)
+        d[f"dct_f64_{norm}"] = D2.transform(d["x_f64"][:64])
+        d[f"idct_f64_{norm}"] = D2.inverse_transform(d["x_f64"][:64])
+    d["x_img"] = image_u8(rng, 64, 48, 3)
+    d["dct_img"] = DCT.transform(_quiet(sh_m.Patcher().patch, d["x_img"]))
+    np.savez_compressed(os.path.join(OUT, "dct.npz"), **d)
+
+    # ---------------------------------------------------------------- quantisation
+    q = {}
+    img1 = image_u8(rng, 64, 64, 1)
+    img3 = image_u8(rng, 64, 64, 3)
+    q["img1"], q["img3"] = img1, img3
+    P = sh_m.Patcher()
+    dct1 = DCT.transform(P.patch(img1))
+    dct3 = DCT.transform(P.patch(img3))
+    q["scales"] = np.array([1.0, 0.5, 0.15, 2.0, 0.07])
+    for i, s in enumerate(q["scales"]):
+        Q = pq_m.PatchQuant(quantization_scale=float(s))
+        q[f"table_{i}"] = Q.get_quantization_table()
+        q[f"q1_{i}"] = Q.quantize(dct1)
+        q[f"q3_{i}"] = Q.quantize(dct3)
+        q[f"dq1_{i}"] = Q.dequantize(q[f"q1_{i}"])
+        q[f"dq3_{i}"] = Q.dequantize(q[f"q3_{i}"])
+        q[f"idq3_{i}"] = DCT.inverse_transform(q[f"dq3_{i}"])
+    Q1 = pq_m.PatchQuant(quantization_scale=1.0)
+    q["raw_q3"] = Q1.quantize(P.patch(img3))                    # tests/ch3.py:37-40 shape
+    q["raw_dq3"] = Q1.dequantize(q["raw_q3"])
+    f32in = DCT.transform(P.patch(img3).astype(np.float32))
+    q["f32_dct3"] = f32in
+    q["f32_q3"] = Q1.quantize(f32in)
+    q["blk88"] = d["dct_u8"][5]
+    q["blk88_q"] = Q1.quantize(q["blk88"])                       # -> (1,1,3,8,8)
+    q["blk388"] = DCT.transform(img3[:8, :8, :].transpose(2, 0, 1).astype(np.float32))
+    q["blk388_q"] = Q1.quantize(q["blk388"])
+    # E3-1_claude.py path: float32 block-of-3 quantised with a float32 DCT
+    q["ties_in"] = (np.arange(-64, 64, dtype=np.float64).reshape(2, 1, 1, 8, 8) * 8.0)
+    q["ties_q"] = Q1.quantize(q["ties_in"])
+    np.savez_compressed(os.path.join(OUT, "quant.npz"), **q)
+
+    # ---------------------------------------------------------------- zig-zag
+    z = {}
+    Z = sh_m.ZigZag()
+    z["x5"] = rng.integers(-500, 500, (3, 2, 3, 8, 8)).astype(np.int32)
+    z["flat"] = _quiet(Z.flatten, z["x5"])
+    z["unflat"] = _quiet(Z.unflatten, z["flat"])
+    z["x5_f64"] = rng.normal(size=(2, 2, 1, 8, 8))
+    z["flat_f64"] = _quiet(Z.flatten, z["x5_f64"])
+    z["x5_i16"] = rng.integers(-500, 500, (2, 2, 1, 8, 8)).astype(np.int16)
+    z["flat_i16"] = _quiet(Z.flatten, z["x5_i16"])
+    z["blk"] = rng.integers(0, 1000, (8, 8))
+    z["scan"] = zz_m.zigzag_scan(z["blk"])
+    z["order"] = Z.zigzag_order
+    np.savez_compressed(os.path.join(OUT, "zigzag.npz"), **z)
+
+    # ---------------------------------------------------------------- motion
+    m = {}
+
+    def me(name, ref, cur, sr):
+        M = mo_m.MotionCompensator(search_range=sr)
+        m[f"{name}_ref"], m[f"{name}_cur"] = ref, cur
+        m[f"{name}_sr"] = np.array(sr)
+        m[f"{name}_mv"] = M.compute_motion_vector(ref, cur)
+
+    base = image_u8(rng, 96, 96, 1)[..., 0]
+    shifted = np.roll(base, (3, -2), axis=(0, 1))
+    me("shift_f64_sr4", base[:64, :64].astype(np.float64), shifted[:64, :64].astype(np.float64), 4)
+    me("shift_f64_sr16", base[:64, :80].astype(np.float64), shifted[:64, :80].astype(np.float64), 16)
+    me("flat_sr4", np.zeros((16, 16)), np.zeros((16, 16)), 4)
+    nz = rng.normal(128, 40, (96, 80))
+    me("nonint_f64_sr4", nz, np.roll(nz, (1, 2), axis=(0, 1)) + rng.normal(0, 0.3, (96, 80)), 4)
+    me("f32_sr4", nz.astype(np.float32)[:64, :64],
+       (np.roll(nz, (-2, 1), axis=(0, 1)) + rng.normal(0, 0.3, (96, 80))).astype(np.float32)[:64, :64], 4)
+    me("u8mod_sr4", base[:64, :64], shifted[:64, :64], 4)
+    me("u8mod_sr7", base[:48, :56], np.roll(base, (5, 4), axis=(0, 1))[:48, :56], 7)
+    me("i16_sr4", (base[:48, :48].astype(np.int16) * 97), (shifted[:48, :48].astype(np.int16) * 89), 4)
+    me("i32_sr3", base[:40, :40].astype(np.int32) * 1000003, shifted[:40, :40].astype(np.int32) * 999983, 3)
+    # order-adversarial: 8-periodic reference -> every candidate window holds the same
+    # multiset of values, so the winner is decided by the rounding of the summation order
+    vals = np.array([0.1, 0.3, 0.7, 1.1, 1.3, 1.7, 2.9, 3.1])
+    pat = vals[rng.integers(0, 8, (8, 8))]
+    per = np.tile(pat, (6, 6))
+    me("periodic_f64_sr8", per, np.full((48, 48), 0.05), 8)
+    me("periodic_f32_sr8", per.astype(np.float32), np.full((48, 48), 0.05, np.float32), 8)
+    me("periodic2_f64_sr5", per[:40, :40] * 1.7, np.full((40, 40), 0.3), 5)
+    # motion compensation (including decoded indices that point out of the frame)
+    M4 = mo_m.MotionCompensator(search_range=4)
+    mv = m["shift_f64_sr4_mv"].copy()
+    mv[0, 0, 0] = 0
+    mv[-1, -1, 0] = 80
+    m["mc_mv"] = mv
+    m["mc_ref1"] = base[:64, :64, None].astype(np.float64)
+    m["mc_out1"] = M4.reconstruct_with_motion_vector(m["mc_ref1"], mv)
+    m["mc_ref3"] = image_u8(rng, 64, 64, 3)
+    m["mc_out3"] = M4.reconstruct_with_motion_vector(m["mc_ref3"], mv)
+    np.savez_compressed(os.path.join(OUT, "motion.npz"), **m)
+
+    # ---------------------------------------------------------------- fused intra chain
+    p = {}
+    Q = pq_m.PatchQuant(quantization_scale=0.5)
+    for C in (1, 3):
+        img = image_u8(rng, 48, 64, C)
+        blocks = DCT.transform(P.patch(img))
+        qq = Q.quantize(blocks)
+        p[f"img{C}"] = img
+        p[f"q{C}"] = qq
+        p[f"zz{C}"] = _quiet(sh_m.ZigZag().flatten, qq)
+        p[f"rec{C}"] = DCT.inverse_transform(Q.dequantize(_quiet(sh_m.ZigZag().unflatten, p[f"zz{C}"])))
+    np.savez_compressed(os.path.join(OUT, "intra.npz"), **p)
+    for f in sorted(os.listdir(OUT)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+if __name__ == "__main__":
+    sys.exit(main())

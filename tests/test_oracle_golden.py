@@ -1,0 +1,118 @@
+"""Pin the CPU oracle (oracle/ivc_oracle.py) against the golden vectors the reference itself
+produced (tests/golden/make_golden.py).  Bit-exact comparisons throughout."""
+import numpy as np
+import pytest
+
+from oracle import ivc_oracle as O
+
+
+def bits_equal(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.dtype == b.dtype and a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def test_dct_golden(golden):
+    d = golden("dct")
+    assert bits_equal(O.dct_transform(d["x_u8"]), d["dct_u8"])
+    assert bits_equal(O.dct_transform(d["x_f64"]), d["dct_f64"])
+    assert bits_equal(O.dct_inverse(d["x_f64"]), d["idct_f64"])
+    assert bits_equal(O.dct_transform(d["x_f32"]), d["dct_f32"])
+    assert bits_equal(O.dct_inverse(d["x_f32"]), d["idct_f32"])
+    assert bits_equal(O.dct_inverse(d["x_i32"]), d["idct_i32"])
+    assert bits_equal(O.dct_transform(d["x_i16"]), d["dct_i16"])
+    for norm in ("backward", "forward"):
+        assert bits_equal(O.dct_transform(d["x_f64"][:64], norm), d[f"dct_f64_{norm}"])
+        assert bits_equal(O.dct_inverse(d["x_f64"][:64], norm), d[f"idct_f64_{norm}"])
+    assert bits_equal(O.dct_transform(O.patch(d["x_img"])), d["dct_img"])
+
+
+def test_quant_golden(golden):
+    q = golden("quant")
+    d1 = O.dct_transform(O.patch(q["img1"]))
+    d3 = O.dct_transform(O.patch(q["img3"]))
+    for i, s in enumerate(q["scales"]):
+        s = float(s)
+        assert bits_equal(O.quant_table(s), q[f"table_{i}"])
+        assert bits_equal(O.quantize(d1, s), q[f"q1_{i}"])
+        assert bits_equal(O.quantize(d3, s), q[f"q3_{i}"])
+        assert bits_equal(O.dequantize(q[f"q1_{i}"], s), q[f"dq1_{i}"])
+        assert bits_equal(O.dequantize(q[f"q3_{i}"], s), q[f"dq3_{i}"])
+        assert bits_equal(O.dct_inverse(q[f"dq3_{i}"]), q[f"idq3_{i}"])
+    assert bits_equal(O.quantize(O.patch(q["img3"])), q["raw_q3"])
+    assert bits_equal(O.dequantize(q["raw_q3"]), q["raw_dq3"])
+    assert bits_equal(O.quantize(q["f32_dct3"]), q["f32_q3"])
+    assert bits_equal(O.quantize(q["blk88"]), q["blk88_q"])
+    assert O.quantize(q["blk88"]).shape == (1, 1, 3, 8, 8)
+    assert bits_equal(O.quantize(q["blk388"]), q["blk388_q"])
+    assert bits_equal(O.quantize(q["ties_in"]), q["ties_q"])
+
+
+def test_zigzag_golden(golden):
+    z = golden("zigzag")
+    assert np.array_equal(z["order"], O.ZZ_ORDER)
+    assert bits_equal(O.zigzag_flatten(z["x5"]), z["flat"])
+    assert bits_equal(O.zigzag_unflatten(z["flat"]), z["unflat"])
+    assert bits_equal(O.zigzag_flatten(z["x5_f64"]), z["flat_f64"])
+    assert bits_equal(O.zigzag_flatten(z["x5_i16"]), z["flat_i16"])
+    assert bits_equal(O.zigzag_scan(z["blk"]), z["scan"])
+
+
+ME_CASES = ["shift_f64_sr4", "shift_f64_sr16", "flat_sr4", "nonint_f64_sr4", "f32_sr4",
+            "u8mod_sr4", "u8mod_sr7", "i16_sr4", "i32_sr3", "periodic_f64_sr8",
+            "periodic_f32_sr8", "periodic2_f64_sr5"]
+
+
+@pytest.mark.parametrize("case", ME_CASES)
+def test_motion_golden(golden, case):
+    m = golden("motion")
+    ref, cur, sr = m[f"{case}_ref"], m[f"{case}_cur"], int(m[f"{case}_sr"])
+    assert bits_equal(O.motion_vectors(ref, cur, sr), m[f"{case}_mv"])
+    if ref.size <= 64 * 64 and sr <= 4:
+        assert bits_equal(O.motion_vectors_loop(ref, cur, sr), m[f"{case}_mv"])
+
+
+def test_motion_flat_tiebreak(golden):
+    m = golden("motion")
+    assert m["flat_sr4_mv"][..., 0].tolist() == [[40, 36], [4, 0]]
+
+
+def test_mc_golden(golden):
+    m = golden("motion")
+    assert bits_equal(O.motion_compensate(m["mc_ref1"], m["mc_mv"], 4), m["mc_out1"])
+    assert bits_equal(O.motion_compensate(m["mc_ref3"], m["mc_mv"], 4), m["mc_out3"])
+
+
+def test_intra_golden(golden):
+    p = golden("intra")
+    for C in (1, 3):
+        assert bits_equal(O.intra_encode(p[f"img{C}"], 0.5), p[f"q{C}"])
+        assert bits_equal(O.intra_encode(p[f"img{C}"], 0.5, zigzag=True), p[f"zz{C}"])
+        assert bits_equal(O.intra_decode(p[f"zz{C}"], 0.5, unzigzag=True), p[f"rec{C}"])
+
+
+@pytest.mark.parametrize("case", ME_CASES)
+def test_c_oracle_motion_golden(golden, case):
+    from oracle import c_motion_vectors
+    m = golden("motion")
+    ref, cur, sr = m[f"{case}_ref"], m[f"{case}_cur"], int(m[f"{case}_sr"])
+    cur = cur.astype(np.result_type(ref.dtype, cur.dtype))
+    ref = ref.astype(cur.dtype)
+    assert bits_equal(c_motion_vectors(ref, cur, sr).astype(int), m[f"{case}_mv"])
+
+
+def test_c_oracle_exact_u8_equals_f64(golden):
+    from oracle import c_motion_vectors
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, 256, (64, 72), dtype=np.uint8)
+    b = np.roll(a, (2, -3), axis=(0, 1))
+    b[::5] = rng.integers(0, 256, b[::5].shape)
+    ref = O.motion_vectors(a.astype(np.float64), b.astype(np.float64), 6)
+    assert np.array_equal(c_motion_vectors(a, b, 6, exact_u8=True), ref)
+    assert np.array_equal(c_motion_vectors(a, b, 6, rows=(2, 5)), O.motion_vectors(a, b, 6)[2:5])
+
+
+def test_c_oracle_mc_golden(golden):
+    from oracle import c_motion_compensate
+    m = golden("motion")
+    assert bits_equal(c_motion_compensate(m["mc_ref1"], m["mc_mv"], 4), m["mc_out1"])
+    assert bits_equal(c_motion_compensate(m["mc_ref3"], m["mc_mv"], 4), m["mc_out3"])
