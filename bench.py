@@ -1,0 +1,302 @@
+"""Benchmark of the ivclab block-codec hot path on MI355X (contract: one JSON line on rank 0).
+
+Workload (BASELINE.json configs[2], the metric's "4K intra DCT+quant" half): a batch of 256
+synthetic 3840x2160 luma frames per GPU, resident in HBM, through the fused
+patch -> DCT-II -> quantise kernel (reference-equivalent output: [F,270,480,3,64] int32,
+the C = 1 -> 3-plane broadcast of patchquant.py:59).  One step = one pass over the batch.
+Multi-GPU: one process per GPU, frames sharded (each rank owns its own 256 frames, weak
+scaling); after the timed steps each rank histograms its symbols and the ranks exchange
+them with one all-gather (the global Huffman table's input).
+
+The metric's other half ("+-16 full-search ME", configs[3]: 1080p x 300 frames, ME +
+MC + residual DCT + quantise) is measured in the same run and reported under "inter".
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--no-inter] [--no-cpu]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+INT_VALU_PEAK_TOPS = 78.6      # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, 32-bit integer ops/s
+HIST_LO, HIST_BINS = -4096, 8192
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        return dist, rank, world, local
+    torch.cuda.set_device(0)
+    return None, 0, 1, 0
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, v):
+    if dist is None:
+        return v
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+# ---------------------------------------------------------------- synthetic frames ------
+def intra_frames(F, H, W, seed, dev):
+    """Per 8x8 block: ~50% uniform noise, 25% flat (DC ties), 25% ramps; seeded, on device."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    out = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
+    h, w = H // 8, W // 8
+    ii = torch.arange(8, device=dev)
+    ramp = (ii[:, None] + ii[None, :]).to(torch.int16)                     # [8, 8]
+    for f in range(F):
+        x = torch.randint(0, 256, (H, W), dtype=torch.uint8, device=dev, generator=g)
+        kind = torch.randint(0, 4, (h, 1, w, 1), device=dev, generator=g)
+        base = torch.randint(0, 256, (h, 1, w, 1), dtype=torch.int16, device=dev, generator=g)
+        slope = torch.randint(1, 17, (h, 1, w, 1), dtype=torch.int16, device=dev, generator=g)
+        xb = x.view(h, 8, w, 8)
+        flat = base.expand(h, 8, w, 8).to(torch.uint8)
+        rmp = (ramp.view(1, 8, 1, 8) * slope).clamp(0, 255).to(torch.uint8)
+        xb = torch.where(kind == 0, flat, xb)
+        xb = torch.where(kind == 1, rmp.expand(h, 8, w, 8), xb)
+        out[f] = xb.reshape(H, W)
+    return out
+
+
+def inter_frames(F, H, W, seed, dev):
+    """Smooth base texture shifted by (dy, dx) = ((f % 7) - 3, (2f % 9) - 4) plus +-2 noise
+    (SURVEY §8d cfg4), so consecutive frames differ by a motion within +-16."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    P = 16
+    lo = torch.randint(0, 256, (1, 1, (H + 2 * P) // 4 + 2, (W + 2 * P) // 4 + 2),
+                       device=dev, generator=g).float()
+    base = torch.nn.functional.interpolate(lo, scale_factor=4, mode="bilinear", align_corners=False)
+    base = base[0, 0, :H + 2 * P, :W + 2 * P]
+    base = base + torch.randint(-12, 13, base.shape, device=dev, generator=g).float()
+    out = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
+    for f in range(F):
+        dy, dx = (f % 7) - 3, (2 * f % 9) - 4
+        fr = base[P + dy:P + dy + H, P + dx:P + dx + W]
+        fr = fr + torch.randint(-2, 3, (H, W), device=dev, generator=g).float()
+        out[f] = fr.round().clamp(0, 255).to(torch.uint8)
+    return out
+
+
+# ---------------------------------------------------------------- timing ----------------
+def timed(dist, fn, steps, warmup):
+    """W untimed steps, then exactly K steps bracketed by barrier + synchronize; returns
+    (max-over-ranks wall seconds, per-step device-event ms of fn's kernels)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    barrier(dist)
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record()
+    for _ in range(steps):
+        fn()
+    ev1.record()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier(dist)
+    wall = max_over_ranks(dist, t1 - t0)
+    return wall, ev0.elapsed_time(ev1) / steps
+
+
+def cpu_baseline_intra(frames_host, budget_s=12.0):
+    """Oracle (NumPy/SciPy restatement of the reference, single thread, as the reference
+    runs) on whole 4K frames until ~budget_s of CPU work; returns Mpx/s and frames done."""
+    from oracle import ivc_oracle as O
+    n, t0 = 0, time.perf_counter()
+    while n < len(frames_host):
+        O.intra_encode(frames_host[n][..., None], 1.0)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    H, W = frames_host[0].shape
+    return n * H * W / dt / 1e6, n, dt
+
+
+def cpu_baseline_me(frames_host, sr, budget_s=10.0):
+    """The reference's literal ME loop (oracle motion_vectors_loop on float64 frames) on a
+    stripe of block rows of one 1080p pair, extrapolated per valid candidate."""
+    from oracle import ivc_oracle as O
+    a = frames_host[0].astype(np.float64)
+    b = frames_host[1].astype(np.float64)
+    H, W = a.shape
+    # a 32-row sub-frame from the middle of the pair (4 block rows x W)
+    sub_h = 32
+    y0 = (H // 2) // 8 * 8
+    ra, rb = a[y0:y0 + sub_h], b[y0:y0 + sub_h]
+    t0 = time.perf_counter()
+    O.motion_vectors_loop(ra, rb, sr)
+    dt = time.perf_counter() - t0
+    n = 2 * sr + 1
+
+    def valid_count(h, w):
+        by = np.arange(h // 8) * 8
+        bx = np.arange(w // 8) * 8
+        d = np.arange(-sr, sr + 1)
+        vy = ((by[:, None] + d[None]) >= 0) & ((by[:, None] + d[None] + 8) <= h)
+        vx = ((bx[:, None] + d[None]) >= 0) & ((bx[:, None] + d[None] + 8) <= w)
+        return int(vy.sum(1).sum() * vx.sum(1).sum())
+
+    per_cand = dt / valid_count(sub_h, W)
+    frame_s = per_cand * valid_count(H, W)
+    return H * W / frame_s / 1e6, per_cand, n
+
+
+# ---------------------------------------------------------------- main ------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames", type=int, default=256)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--inter-frames", type=int, default=300)
+    ap.add_argument("--inter-steps", type=int, default=3)
+    ap.add_argument("--sr", type=int, default=16)
+    ap.add_argument("--zigzag", action="store_true")
+    ap.add_argument("--no-inter", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    dist, rank, world, local = dist_setup(args.gpus)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    import ivclab_amd.device as D
+    from ivclab_amd import PatchQuant
+    table = PatchQuant(1.0).get_quantization_table()
+
+    # ---- cfg3: 4K intra DCT + quant -------------------------------------------------------
+    F, H, W = args.frames, args.height, args.width
+    frames = intra_frames(F, H, W, seed=3 + 1000 * rank, dev=dev).view(F, H, W, 1)
+    out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+
+    def step():
+        D.intra_encode(frames, table, out, zigzag=args.zigzag)
+
+    wall, kern_ms = timed(dist, step, args.steps, args.warmup)
+    px_step = F * H * W
+    value = world * px_step * args.steps / wall / 1e6
+    algo_bytes = px_step * 13                        # 1 B u8 in + 3 x 4 B int32 out per px
+    achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+
+    # exchange for the global Huffman table: per-rank histogram + one all-gather
+    hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    t_ex = time.perf_counter()
+    D.histogram(out.view(-1), HIST_LO, hist)
+    if dist is not None:
+        gathered = torch.empty((world, HIST_BINS), dtype=torch.int64, device=dev)
+        dist.all_gather_into_tensor(gathered, hist)
+        ghist = gathered.sum(0)
+    else:
+        ghist = hist
+    torch.cuda.synchronize()
+    exchange_ms = (time.perf_counter() - t_ex) * 1e3
+    total_syms = int(ghist.sum().item())
+
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_intra_latest.json")
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            rec = json.load(fh)
+        if rec.get("frames") == F and rec.get("H") == H and rec.get("W") == W:
+            traffic = rec.get("hbm_bytes_per_launch")
+
+    result = {
+        "metric": "Mpixels/s: 4K intra DCT+quant and ±16 full-search ME, 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "Mpixels/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (seeded on-device 4K luma: 50% noise / 25% flat / 25% ramp blocks)",
+        "config": {"workload": f"cfg3: {F} x {W}x{H} luma u8 per GPU, fused patch->DCT->quant "
+                               f"(scale 1.0, [F,h,w,3,64] int32{', zig-zag' if args.zigzag else ''})",
+                   "frames_per_gpu": F, "height": H, "width": W, "parallelism": f"frame-shard x{world}"},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": traffic, "kernel": "fused_encode_kernel<u8,f64,C=1>",
+                     "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": algo_bytes},
+        "exchange": {"histogram_bins": HIST_BINS, "symbols": total_syms, "ms": round(exchange_ms, 3),
+                     "collective": "all_gather_into_tensor (RCCL)" if dist is not None else "none (1 rank)"},
+    }
+    del out, frames
+    torch.cuda.empty_cache()
+
+    # ---- cfg4: 1080p x 300, +-16 ME + MC + residual DCT + quant ------------------------------
+    if not args.no_inter:
+        Fi, Hi, Wi, sr = args.inter_frames, 1080, 1920, args.sr
+        seq = inter_frames(Fi, Hi, Wi, seed=4 + 1000 * rank, dev=dev)
+        mv = torch.empty((Fi - 1, Hi // 8, Wi // 8), dtype=torch.int64, device=dev)
+        q = torch.empty((Fi - 1, Hi // 8, Wi // 8, 3, 64), dtype=torch.int32, device=dev)
+
+        def istep():
+            D.inter_encode(seq, sr, table, mv, q, zigzag=args.zigzag)
+
+        iwall, ims = timed(dist, istep, args.inter_steps, 1)
+        ipx = (Fi - 1) * Hi * Wi
+        ivalue = world * ipx * args.inter_steps / iwall / 1e6
+        result["inter"] = {
+            "metric": "Mpixels/s: 1080p +-16 full-search ME + MC + residual DCT+quant",
+            "value": round(ivalue, 1), "unit": "Mpixels/s",
+            "ms_per_step": round(iwall / args.inter_steps * 1e3, 3),
+            "config": {"workload": f"cfg4: {Fi} frames 1920x1080 u8 luma per GPU, sr={sr}, "
+                                   "ME against the previous source frame (open loop)"},
+        }
+        if rank == 0 and not args.no_cpu:
+            host = seq[:2].cpu().numpy()
+            mpx, per_cand, _ = cpu_baseline_me(host, sr)
+            result["inter"]["cpu_baseline"] = {
+                "value": round(mpx, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+                "sample": f"reference ME loop (oracle motion_vectors_loop, float64) on 2 block rows "
+                          f"of a 1080p pair at sr={sr}; {per_cand * 1e6:.3f} us per valid candidate, "
+                          "extrapolated by exact valid-candidate count"}
+        del seq, mv, q
+        torch.cuda.empty_cache()
+
+    if rank == 0 and not args.no_cpu:
+        host = intra_frames(40, H, W, seed=3, dev=dev).cpu().numpy()
+        mpx, n, dt = cpu_baseline_intra(host)
+        result["cpu_baseline"] = {
+            "value": round(mpx, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
+            "sample": f"oracle (scipy dct + np.round quantise, the reference's algorithm) on {n} "
+                      f"whole {W}x{H} frames of the same generator, {dt:.1f} s single-threaded"}
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

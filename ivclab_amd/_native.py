@@ -1,0 +1,148 @@
+"""ctypes binding of libivc.so (the C-ABI declared in include/ivc.h).
+
+There is no CPU fallback: if the shared library is missing, was built for another
+architecture, or no gfx950 device is visible, every hot-path call raises.  The library is
+built in-tree by `python -m ivclab_amd.build` (or __graft_entry__.build()).
+"""
+from __future__ import annotations
+
+import ctypes as _ct
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "libivc.so")
+
+# ivc_dtype codes (include/ivc.h)
+DTYPE_CODE = {
+    np.dtype(np.uint8): 1, np.dtype(np.int8): 2, np.dtype(np.uint16): 3,
+    np.dtype(np.int16): 4, np.dtype(np.uint32): 5, np.dtype(np.int32): 6,
+    np.dtype(np.uint64): 7, np.dtype(np.int64): 8, np.dtype(np.float32): 9,
+    np.dtype(np.float64): 10,
+}
+F32, F64 = 9, 10
+NORM_CODE = {None: 0, "backward": 0, "ortho": 1, "forward": 2}
+ME_NUMPY, ME_EXACT_U8 = 0, 1
+
+E_ARG, E_DTYPE, E_SHAPE, E_DEVICE, E_NOMEM = -1, -2, -3, -4, -5
+
+
+class IvcError(RuntimeError):
+    """Device-side failure reported by libivc (status IVC_E_DEVICE / IVC_E_NOMEM)."""
+
+
+_P, _I, _L = _ct.c_void_p, _ct.c_int, _ct.c_int64
+_SIGS = {
+    "ivc_last_error": ([], _ct.c_char_p),
+    "ivc_version": ([], _I),
+    "ivc_device_count": ([], _I),
+    "ivc_set_device": ([_I], _I),
+    "ivc_device_ok": ([], _I),
+    "ivc_release_scratch": ([], _I),
+    "ivc_dct8x8": ([_P, _I, _L, _P, _I, _I, _I], _I),
+    "ivc_dct8x8_dev": ([_P, _I, _L, _P, _I, _I, _I, _P], _I),
+    "ivc_quantize": ([_P, _I, _L, _I, _P, _I, _P], _I),
+    "ivc_quantize_dev": ([_P, _I, _L, _I, _P, _I, _P, _P], _I),
+    "ivc_dequantize": ([_P, _I, _L, _I, _P, _I, _P], _I),
+    "ivc_dequantize_dev": ([_P, _I, _L, _I, _P, _I, _P, _P], _I),
+    "ivc_zigzag": ([_P, _L, _L, _I, _I, _P], _I),
+    "ivc_zigzag_dev": ([_P, _L, _L, _I, _I, _P, _P], _I),
+    "ivc_intra_encode": ([_P, _I, _L, _L, _L, _I, _P, _I, _I, _P], _I),
+    "ivc_intra_encode_dev": ([_P, _I, _L, _L, _L, _I, _P, _I, _I, _P, _P, _ct.c_int32,
+                              _ct.c_int32, _P], _I),
+    "ivc_intra_decode": ([_P, _L, _P, _I, _I, _P], _I),
+    "ivc_intra_decode_dev": ([_P, _L, _P, _I, _I, _P, _P], _I),
+    "ivc_motion_estimate": ([_P, _P, _I, _L, _L, _L, _I, _I, _P], _I),
+    "ivc_motion_estimate_dev": ([_P, _P, _I, _L, _L, _L, _I, _I, _P, _P], _I),
+    "ivc_motion_compensate": ([_P, _I, _L, _L, _L, _L, _P, _I, _P], _I),
+    "ivc_motion_compensate_dev": ([_P, _I, _L, _L, _L, _L, _P, _I, _P, _P], _I),
+    "ivc_inter_encode_dev": ([_P, _L, _L, _L, _I, _P, _I, _I, _P, _P, _P], _I),
+    "ivc_histogram_i32": ([_P, _L, _ct.c_int32, _ct.c_int32, _P], _I),
+    "ivc_histogram_i32_dev": ([_P, _L, _ct.c_int32, _ct.c_int32, _P, _P], _I),
+}
+EXPORTS = tuple(_SIGS)
+
+_lib = None
+_lock = threading.Lock()
+_device_checked = False
+
+
+def _share_torch_hip_runtime() -> None:
+    """Bind libivc to the HIP runtime torch ships, when torch is installed.
+
+    torch-ROCm bundles its own libamdhip64 / libhsa-runtime64 (same SONAMEs as /opt/rocm's).
+    Two HIP runtimes in one process cannot both own the GPU: whichever initialises second
+    sees no device.  Loading torch's copies first (RTLD_GLOBAL) makes libivc's DT_NEEDED
+    entries resolve to them by SONAME, so the process has exactly one runtime whatever the
+    import order.  IVC_HIP_RUNTIME=system keeps /opt/rocm's runtime instead.
+    """
+    if os.environ.get("IVC_HIP_RUNTIME", "") == "system":
+        return
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    tlib = os.path.join(os.path.dirname(spec.origin), "lib")
+    for name in ("libhsa-runtime64.so", "libamdhip64.so"):
+        p = os.path.join(tlib, name)
+        if os.path.exists(p):
+            _ct.CDLL(p, mode=_ct.RTLD_GLOBAL)
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libivc.so and declare its signatures (no device is touched)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(path):
+                raise ImportError(
+                    f"ivclab_amd: native library {path} is missing; build it with "
+                    "`python -m ivclab_amd.build` (hipcc --offload-arch=gfx950)")
+            _share_torch_hip_runtime()
+            lib = _ct.CDLL(path)
+            for name, (args, res) in _SIGS.items():
+                fn = getattr(lib, name)
+                fn.argtypes = args
+                fn.restype = res
+            _lib = lib
+    return _lib
+
+
+def lib():
+    """The loaded library, after checking once that a gfx950 device is present."""
+    global _device_checked
+    L = load_library()
+    if not _device_checked:
+        if L.ivc_device_count() < 1:
+            raise IvcError("ivclab_amd: no HIP device visible; the block-codec path runs only "
+                           "on an MI355X (gfx950) — there is no CPU fallback")
+        if not L.ivc_device_ok():
+            raise IvcError("ivclab_amd: current HIP device is not gfx950 (MI355X)")
+        _device_checked = True
+    return L
+
+
+def check(status: int, what: str = "ivc") -> None:
+    """Map a libivc status to the exception class NumPy would raise for the same misuse."""
+    if status == 0:
+        return
+    msg = (load_library().ivc_last_error() or b"").decode(errors="replace")
+    if status in (E_SHAPE, E_DTYPE, E_ARG):
+        raise ValueError(f"{what}: {msg}")
+    if status == E_NOMEM:
+        raise MemoryError(f"{what}: {msg}")
+    raise IvcError(f"{what}: {msg}")
+
+
+def ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+def table_arg(table: np.ndarray) -> np.ndarray:
+    """3x8x8 table as 192 float64 values (exact for float32/float64 tables)."""
+    t = np.ascontiguousarray(table, dtype=np.float64).reshape(-1)
+    if t.size != 192:
+        raise ValueError("quantization table must hold 3 x 8 x 8 values")
+    return t

@@ -1,0 +1,492 @@
+// ivc_capi.hip — the extern "C" boundary of libivc.so (declared in include/ivc.h).
+//
+// Validates arguments the way the reference's NumPy code would fail (shape / dtype), maps
+// launch errors to status codes with a per-thread message, and implements the host-buffer
+// entry points by staging through per-device scratch memory on a library-owned stream.
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+
+#include "ivc_internal.h"
+
+using namespace ivc;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+int fail_hip(hipError_t e, const char* what) {
+  return fail(IVC_E_DEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+bool valid_dtype(int dt) { return dt >= IVC_U8 && dt <= IVC_F64; }
+bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// ---------------------------------------------------------------- device context -------
+constexpr int kMaxDev = 64;
+constexpr int kSlots = 6;
+struct DevCtx {
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  void* slot[kSlots] = {};
+  size_t cap[kSlots] = {};
+};
+DevCtx g_ctx[kMaxDev];
+
+int current_device(int* dev) {
+  hipError_t e = hipGetDevice(dev);
+  if (e != hipSuccess) return fail_hip(e, "hipGetDevice");
+  if (*dev < 0 || *dev >= kMaxDev) return fail(IVC_E_DEVICE, "device index out of range");
+  return IVC_OK;
+}
+
+// Host-buffer call: lock the device context, stage inputs, run, copy outputs back.
+struct Staging {
+  DevCtx* ctx = nullptr;
+  int next = 0;
+  int status = IVC_OK;
+  std::unique_lock<std::mutex> lock;
+
+  int open() {
+    int dev = 0;
+    int rc = current_device(&dev);
+    if (rc) return rc;
+    ctx = &g_ctx[dev];
+    lock = std::unique_lock<std::mutex>(ctx->mu);
+    if (!ctx->stream) {
+      hipError_t e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+      if (e != hipSuccess) return fail_hip(e, "hipStreamCreate");
+    }
+    return IVC_OK;
+  }
+  void* alloc(size_t bytes) {
+    if (status) return nullptr;
+    if (next >= kSlots) { status = fail(IVC_E_ARG, "internal: too many staging buffers"); return nullptr; }
+    const int i = next++;
+    if (bytes == 0) bytes = 16;
+    if (ctx->cap[i] < bytes) {
+      if (ctx->slot[i]) (void)hipFree(ctx->slot[i]);
+      ctx->slot[i] = nullptr;
+      ctx->cap[i] = 0;
+      hipError_t e = hipMalloc(&ctx->slot[i], bytes);
+      if (e != hipSuccess) {
+        status = fail(IVC_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+        return nullptr;
+      }
+      ctx->cap[i] = bytes;
+    }
+    return ctx->slot[i];
+  }
+  void* in(const void* host, size_t bytes) {
+    void* d = alloc(bytes);
+    if (d && bytes) {
+      hipError_t e = hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, ctx->stream);
+      if (e != hipSuccess) status = fail_hip(e, "hipMemcpyAsync H2D");
+    }
+    return d;
+  }
+  int launched(hipError_t e, const char* what) {
+    if (status) return status;
+    if (e == hipErrorInvalidValue) return status = fail(IVC_E_DTYPE, std::string(what) + ": unsupported dtype/argument combination");
+    if (e != hipSuccess) return status = fail_hip(e, what);
+    return IVC_OK;
+  }
+  int out(void* host, const void* dev, size_t bytes) {
+    if (status) return status;
+    if (bytes) {
+      hipError_t e = hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream);
+      if (e != hipSuccess) return status = fail_hip(e, "hipMemcpyAsync D2H");
+    }
+    return IVC_OK;
+  }
+  int sync() {
+    if (status) return status;
+    hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) return status = fail_hip(e, "hipStreamSynchronize");
+    return IVC_OK;
+  }
+};
+
+int dev_launch(hipError_t e, const char* what) {
+  if (e == hipErrorInvalidValue)
+    return fail(IVC_E_DTYPE, std::string(what) + ": unsupported dtype/argument combination");
+  if (e != hipSuccess) return fail_hip(e, what);
+  return IVC_OK;
+}
+
+int load_table(const double* table, QTab* t) {
+  if (!table) return fail(IVC_E_ARG, "quantization table is NULL");
+  memset(t, 0, sizeof(*t));
+  for (int i = 0; i < 192; ++i) {
+    t->q[i] = table[i];
+    if (!(table[i] == table[i])) return fail(IVC_E_ARG, "quantization table holds NaN");
+  }
+  return IVC_OK;
+}
+
+#define CHECK(cond, code, msg) \
+  do {                         \
+    if (!(cond)) return fail(code, msg); \
+  } while (0)
+#define TRY(x)          \
+  do {                  \
+    int rc_ = (x);      \
+    if (rc_) return rc_; \
+  } while (0)
+
+// ---------------------------------------------------------------- argument checks ------
+int check_dct(int src_dtype, int64_t nblk, int dst_dtype, int norm) {
+  CHECK(valid_dtype(src_dtype), IVC_E_DTYPE, "dct8x8: invalid source dtype");
+  CHECK(dst_dtype == IVC_F32 || dst_dtype == IVC_F64, IVC_E_DTYPE, "dct8x8: output must be float32 or float64");
+  CHECK((dst_dtype == IVC_F32) == (src_dtype == IVC_F32), IVC_E_DTYPE,
+        "dct8x8: scipy computes float32 input in float32 and every other dtype in float64");
+  CHECK(nblk >= 0, IVC_E_SHAPE, "dct8x8: negative block count");
+  CHECK(norm >= 0 && norm <= 2, IVC_E_ARG, "dct8x8: norm must be backward/ortho/forward");
+  return IVC_OK;
+}
+int check_quant(int src_dtype, int64_t nblk, int C, int calc) {
+  CHECK(valid_dtype(src_dtype), IVC_E_DTYPE, "quantize: invalid source dtype");
+  CHECK(C == 1 || C == 3, IVC_E_SHAPE, "quantize: channel axis must broadcast against 3 table planes");
+  CHECK(calc == IVC_F32 || calc == IVC_F64, IVC_E_DTYPE, "quantize: calc dtype must be float32/float64");
+  CHECK(nblk >= 0, IVC_E_SHAPE, "quantize: negative block count");
+  return IVC_OK;
+}
+int check_frames(int64_t nframes, int64_t H, int64_t W, const char* what) {
+  CHECK(nframes >= 0 && H >= 0 && W >= 0, IVC_E_SHAPE, std::string(what) + ": negative size");
+  CHECK(H % 8 == 0 && W % 8 == 0, IVC_E_SHAPE, std::string(what) + ": H and W must be multiples of 8");
+  CHECK(H < (1LL << 30) && W < (1LL << 30), IVC_E_SHAPE, std::string(what) + ": frame too large");
+  return IVC_OK;
+}
+int check_sr(int sr) {
+  CHECK(sr >= 0 && sr <= 4096, IVC_E_ARG, "search_range must be in [0, 4096]");
+  return IVC_OK;
+}
+
+}  // namespace
+
+// ======================================================================================
+extern "C" {
+
+const char* ivc_last_error(void) { return g_err.c_str(); }
+int ivc_version(void) { return 10000; }
+
+int ivc_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+int ivc_set_device(int device) {
+  hipError_t e = hipSetDevice(device);
+  return e == hipSuccess ? IVC_OK : fail_hip(e, "hipSetDevice");
+}
+
+int ivc_device_ok(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
+  return strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
+}
+
+int ivc_release_scratch(void) {
+  int dev = 0;
+  TRY(current_device(&dev));
+  DevCtx& c = g_ctx[dev];
+  std::lock_guard<std::mutex> g(c.mu);
+  for (int i = 0; i < kSlots; ++i) {
+    if (c.slot[i]) (void)hipFree(c.slot[i]);
+    c.slot[i] = nullptr;
+    c.cap[i] = 0;
+  }
+  return IVC_OK;
+}
+
+// ---------------------------------------------------------------- DCT -----------------
+int ivc_dct8x8_dev(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
+                   int inverse, int norm, void* stream) {
+  TRY(check_dct(src_dtype, nblk, dst_dtype, norm));
+  CHECK(aligned16(src) && aligned16(dst), IVC_E_ARG, "dct8x8_dev: pointers must be 16-byte aligned");
+  return dev_launch(launch_dct8x8(src, src_dtype, nblk, dst, dst_dtype, inverse, norm,
+                                  (hipStream_t)stream), "dct8x8");
+}
+
+int ivc_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
+               int inverse, int norm) {
+  TRY(check_dct(src_dtype, nblk, dst_dtype, norm));
+  if (nblk == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t ib = (size_t)nblk * 64 * dtype_size(src_dtype);
+  const size_t ob = (size_t)nblk * 64 * dtype_size(dst_dtype);
+  void* d_in = st.in(src, ib);
+  void* d_out = st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_dct8x8(d_in, src_dtype, nblk, d_out, dst_dtype, inverse, norm,
+                                st.ctx->stream), "dct8x8"));
+  TRY(st.out(dst, d_out, ob));
+  return st.sync();
+}
+
+// ---------------------------------------------------------------- quantisation --------
+int ivc_quantize_dev(const void* src, int src_dtype, int64_t nblk, int C, const double* table,
+                     int calc_dtype, int32_t* dst, void* stream) {
+  TRY(check_quant(src_dtype, nblk, C, calc_dtype));
+  CHECK(aligned16(dst), IVC_E_ARG, "quantize_dev: output must be 16-byte aligned");
+  QTab t;
+  TRY(load_table(table, &t));
+  return dev_launch(launch_quantize(src, src_dtype, nblk, C, t, calc_dtype, dst,
+                                    (hipStream_t)stream), "quantize");
+}
+
+int ivc_quantize(const void* src, int src_dtype, int64_t nblk, int C, const double* table,
+                 int calc_dtype, int32_t* dst) {
+  TRY(check_quant(src_dtype, nblk, C, calc_dtype));
+  QTab t;
+  TRY(load_table(table, &t));
+  if (nblk == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
+  void* d_in = st.in(src, ib);
+  int32_t* d_out = (int32_t*)st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_quantize(d_in, src_dtype, nblk, C, t, calc_dtype, d_out, st.ctx->stream),
+                  "quantize"));
+  TRY(st.out(dst, d_out, ob));
+  return st.sync();
+}
+
+int ivc_dequantize_dev(const void* src, int src_dtype, int64_t nblk, int C, const double* table,
+                       int calc_dtype, int32_t* dst, void* stream) {
+  TRY(check_quant(src_dtype, nblk, C, calc_dtype));
+  CHECK(aligned16(dst), IVC_E_ARG, "dequantize_dev: output must be 16-byte aligned");
+  QTab t;
+  TRY(load_table(table, &t));
+  return dev_launch(launch_dequantize(src, src_dtype, nblk, C, t, calc_dtype, dst,
+                                      (hipStream_t)stream), "dequantize");
+}
+
+int ivc_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const double* table,
+                   int calc_dtype, int32_t* dst) {
+  TRY(check_quant(src_dtype, nblk, C, calc_dtype));
+  QTab t;
+  TRY(load_table(table, &t));
+  if (nblk == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
+  void* d_in = st.in(src, ib);
+  int32_t* d_out = (int32_t*)st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_dequantize(d_in, src_dtype, nblk, C, t, calc_dtype, d_out,
+                                    st.ctx->stream), "dequantize"));
+  TRY(st.out(dst, d_out, ob));
+  return st.sync();
+}
+
+// ---------------------------------------------------------------- zig-zag -------------
+int ivc_zigzag_dev(const void* src, int64_t nrow, int64_t stride, int esize, int inverse,
+                   void* dst, void* stream) {
+  CHECK(esize == 1 || esize == 2 || esize == 4 || esize == 8, IVC_E_DTYPE, "zigzag: element size must be 1, 2, 4 or 8");
+  CHECK(nrow >= 0 && stride >= 64, IVC_E_SHAPE, "zigzag: rows need at least 64 elements");
+  return dev_launch(launch_zigzag(src, nrow, stride, esize, inverse, dst, (hipStream_t)stream),
+                    "zigzag");
+}
+
+int ivc_zigzag(const void* src, int64_t nrow, int64_t stride, int esize, int inverse,
+               void* dst) {
+  CHECK(esize == 1 || esize == 2 || esize == 4 || esize == 8, IVC_E_DTYPE, "zigzag: element size must be 1, 2, 4 or 8");
+  CHECK(nrow >= 0 && stride >= 64, IVC_E_SHAPE, "zigzag: rows need at least 64 elements");
+  if (nrow == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t ib = (size_t)nrow * stride * esize, ob = (size_t)nrow * 64 * esize;
+  void* d_in = st.in(src, ib);
+  void* d_out = st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_zigzag(d_in, nrow, stride, esize, inverse, d_out, st.ctx->stream), "zigzag"));
+  TRY(st.out(dst, d_out, ob));
+  return st.sync();
+}
+
+// ---------------------------------------------------------------- fused intra ---------
+int ivc_intra_encode_dev(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
+                         int C, const double* table, int calc_dtype, int zigzag, int32_t* out,
+                         int64_t* hist, int32_t hist_lo, int32_t nbins, void* stream) {
+  TRY(check_frames(nframes, H, W, "intra_encode"));
+  CHECK(C == 1 || C == 3, IVC_E_SHAPE, "intra_encode: C must be 1 or 3");
+  CHECK(aligned16(img) && aligned16(out), IVC_E_ARG, "intra_encode_dev: pointers must be 16-byte aligned");
+  QTab t;
+  TRY(load_table(table, &t));
+  hipStream_t s = (hipStream_t)stream;
+  TRY(dev_launch(launch_intra_encode(img, dtype, nframes, H, W, C, t, calc_dtype, zigzag, out, s),
+                 "intra_encode"));
+  if (hist) {
+    CHECK(nbins > 0, IVC_E_ARG, "intra_encode: nbins must be positive");
+    TRY(dev_launch(launch_histogram(out, nframes * (H / 8) * (W / 8) * 192, hist_lo, nbins, hist, s),
+                   "histogram"));
+  }
+  return IVC_OK;
+}
+
+int ivc_intra_encode(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W, int C,
+                     const double* table, int calc_dtype, int zigzag, int32_t* out) {
+  TRY(check_frames(nframes, H, W, "intra_encode"));
+  CHECK(C == 1 || C == 3, IVC_E_SHAPE, "intra_encode: C must be 1 or 3");
+  CHECK(valid_dtype(dtype), IVC_E_DTYPE, "intra_encode: invalid dtype");
+  QTab t;
+  TRY(load_table(table, &t));
+  if (nframes * H * W == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t ib = (size_t)(nframes * H * W * C) * dtype_size(dtype);
+  const size_t ob = (size_t)(nframes * (H / 8) * (W / 8)) * 192 * 4;
+  void* d_in = st.in(img, ib);
+  int32_t* d_out = (int32_t*)st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_intra_encode(d_in, dtype, nframes, H, W, C, t, calc_dtype, zigzag, d_out,
+                                      st.ctx->stream), "intra_encode"));
+  TRY(st.out(out, d_out, ob));
+  return st.sync();
+}
+
+int ivc_intra_decode_dev(const int32_t* q, int64_t nblk, const double* table, int calc_dtype,
+                         int unzigzag, double* out, void* stream) {
+  CHECK(nblk >= 0, IVC_E_SHAPE, "intra_decode: negative block count");
+  CHECK(calc_dtype == IVC_F64, IVC_E_DTYPE, "intra_decode: int32 symbols dequantise in float64");
+  CHECK(aligned16(out), IVC_E_ARG, "intra_decode_dev: output must be 16-byte aligned");
+  QTab t;
+  TRY(load_table(table, &t));
+  return dev_launch(launch_intra_decode(q, nblk, t, unzigzag, out, (hipStream_t)stream),
+                    "intra_decode");
+}
+
+int ivc_intra_decode(const int32_t* q, int64_t nblk, const double* table, int calc_dtype,
+                     int unzigzag, double* out) {
+  CHECK(nblk >= 0, IVC_E_SHAPE, "intra_decode: negative block count");
+  CHECK(calc_dtype == IVC_F64, IVC_E_DTYPE, "intra_decode: int32 symbols dequantise in float64");
+  QTab t;
+  TRY(load_table(table, &t));
+  if (nblk == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t ib = (size_t)nblk * 192 * 4, ob = (size_t)nblk * 192 * 8;
+  void* d_in = st.in(q, ib);
+  double* d_out = (double*)st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_intra_decode((const int32_t*)d_in, nblk, t, unzigzag, d_out,
+                                      st.ctx->stream), "intra_decode"));
+  TRY(st.out(out, d_out, ob));
+  return st.sync();
+}
+
+// ---------------------------------------------------------------- motion --------------
+int ivc_motion_estimate_dev(const void* ref, const void* cur, int dtype, int64_t nframes,
+                            int64_t H, int64_t W, int sr, int mode, int64_t* mv, void* stream) {
+  TRY(check_frames(nframes, H, W, "motion_estimate"));
+  TRY(check_sr(sr));
+  CHECK(valid_dtype(dtype), IVC_E_DTYPE, "motion_estimate: invalid dtype");
+  return dev_launch(launch_motion_estimate(ref, cur, dtype, nframes, H, W, sr, mode, mv,
+                                           (hipStream_t)stream), "motion_estimate");
+}
+
+int ivc_motion_estimate(const void* ref, const void* cur, int dtype, int64_t nframes, int64_t H,
+                        int64_t W, int sr, int mode, int64_t* mv) {
+  TRY(check_frames(nframes, H, W, "motion_estimate"));
+  TRY(check_sr(sr));
+  CHECK(valid_dtype(dtype), IVC_E_DTYPE, "motion_estimate: invalid dtype");
+  const int64_t nblk = nframes * (H / 8) * (W / 8);
+  if (nblk == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t fb = (size_t)(nframes * H * W) * dtype_size(dtype), ob = (size_t)nblk * 8;
+  void* d_ref = st.in(ref, fb);
+  void* d_cur = st.in(cur, fb);
+  int64_t* d_mv = (int64_t*)st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_motion_estimate(d_ref, d_cur, dtype, nframes, H, W, sr, mode, d_mv,
+                                         st.ctx->stream), "motion_estimate"));
+  TRY(st.out(mv, d_mv, ob));
+  return st.sync();
+}
+
+int ivc_motion_compensate_dev(const void* ref, int esize, int64_t nframes, int64_t H, int64_t W,
+                              int64_t C, const int64_t* mv, int sr, void* out, void* stream) {
+  TRY(check_frames(nframes, H, W, "motion_compensate"));
+  TRY(check_sr(sr));
+  CHECK(esize == 1 || esize == 2 || esize == 4 || esize == 8, IVC_E_DTYPE, "motion_compensate: element size must be 1, 2, 4 or 8");
+  CHECK(C >= 1, IVC_E_SHAPE, "motion_compensate: C must be >= 1");
+  return dev_launch(launch_motion_compensate(ref, esize, nframes, H, W, C, mv, sr, out,
+                                             (hipStream_t)stream), "motion_compensate");
+}
+
+int ivc_motion_compensate(const void* ref, int esize, int64_t nframes, int64_t H, int64_t W,
+                          int64_t C, const int64_t* mv, int sr, void* out) {
+  TRY(check_frames(nframes, H, W, "motion_compensate"));
+  TRY(check_sr(sr));
+  CHECK(esize == 1 || esize == 2 || esize == 4 || esize == 8, IVC_E_DTYPE, "motion_compensate: element size must be 1, 2, 4 or 8");
+  CHECK(C >= 1, IVC_E_SHAPE, "motion_compensate: C must be >= 1");
+  const size_t fb = (size_t)(nframes * H * W * C) * esize;
+  if (fb == 0) return IVC_OK;
+  const size_t mb = (size_t)(nframes * (H / 8) * (W / 8)) * 8;
+  Staging st;
+  TRY(st.open());
+  void* d_ref = st.in(ref, fb);
+  int64_t* d_mv = (int64_t*)st.in(mv, mb);
+  void* d_out = st.alloc(fb);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_motion_compensate(d_ref, esize, nframes, H, W, C, d_mv, sr, d_out,
+                                           st.ctx->stream), "motion_compensate"));
+  TRY(st.out(out, d_out, fb));
+  return st.sync();
+}
+
+// ---------------------------------------------------------------- fused inter ---------
+int ivc_inter_encode_dev(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W, int sr,
+                         const double* table, int calc_dtype, int zigzag, int64_t* mv,
+                         int32_t* out, void* stream) {
+  TRY(check_frames(nframes, H, W, "inter_encode"));
+  TRY(check_sr(sr));
+  CHECK(calc_dtype == IVC_F64, IVC_E_DTYPE, "inter_encode: float64 residual DCT needs float64 quantisation");
+  CHECK(aligned16(out), IVC_E_ARG, "inter_encode_dev: output must be 16-byte aligned");
+  CHECK(((uintptr_t)frames & 7u) == 0, IVC_E_ARG, "inter_encode_dev: frames must be 8-byte aligned");
+  if (nframes < 2) return IVC_OK;
+  QTab t;
+  TRY(load_table(table, &t));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t HW = H * W;
+  TRY(dev_launch(launch_motion_estimate(frames, frames + HW, IVC_U8, nframes - 1, H, W, sr,
+                                        IVC_ME_EXACT_U8, mv, s), "motion_estimate"));
+  return dev_launch(launch_inter_residual(frames, nframes - 1, H, W, sr, mv, t, zigzag, out, s),
+                    "inter_residual");
+}
+
+// ---------------------------------------------------------------- histogram -----------
+int ivc_histogram_i32_dev(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, int64_t* hist,
+                          void* stream) {
+  CHECK(n >= 0 && nbins > 0, IVC_E_ARG, "histogram: need n >= 0 and nbins > 0");
+  return dev_launch(launch_histogram(sym, n, lo, nbins, hist, (hipStream_t)stream), "histogram");
+}
+
+int ivc_histogram_i32(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, int64_t* hist) {
+  CHECK(n >= 0 && nbins > 0, IVC_E_ARG, "histogram: need n >= 0 and nbins > 0");
+  Staging st;
+  TRY(st.open());
+  const size_t hb = (size_t)nbins * 8;
+  void* d_sym = st.in(sym, (size_t)n * 4);
+  int64_t* d_hist = (int64_t*)st.in(hist, hb);  // accumulate onto the caller's counts
+  if (st.status) return st.status;
+  TRY(st.launched(launch_histogram((const int32_t*)d_sym, n, lo, nbins, d_hist, st.ctx->stream),
+                  "histogram"));
+  TRY(st.out(hist, d_hist, hb));
+  return st.sync();
+}
+
+}  // extern "C"

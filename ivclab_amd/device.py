@@ -1,0 +1,86 @@
+"""Device-resident entry points (torch tensors already in HBM), used by bench.py and the
+multi-GPU path.  Thin wrappers over the *_dev functions of include/ivc.h: pointers come
+from tensor.data_ptr(), work is enqueued on the given (default: current) torch stream and
+nothing is synchronised.  torch is plumbing here (allocation, streams, RCCL); every byte
+of the hot path is computed by libivc's kernels.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _native as N
+
+
+def _stream(stream):
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def _dtype_code(t) -> int:
+    import torch
+    m = {torch.uint8: 1, torch.int8: 2, torch.int16: 4, torch.int32: 6, torch.int64: 8,
+         torch.float32: 9, torch.float64: 10}
+    if t.dtype not in m:
+        raise TypeError(f"unsupported tensor dtype {t.dtype}")
+    return m[t.dtype]
+
+
+def _contig(t, name):
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    return t
+
+
+def quant_table(scale=1.0) -> np.ndarray:
+    """The reference's default scaled table (PatchQuant(scale).get_quantization_table())."""
+    from .quantization import PatchQuant
+    return N.table_arg(PatchQuant(scale).get_quantization_table())
+
+
+def intra_encode(img, table, out, zigzag=False, hist=None, hist_lo=0, stream=None):
+    """img [F, H, W, C] (uint8/float32/float64) -> out [F, H/8, W/8, 3, 64] int32:
+    quantize(DCT(patch(img))) (+ zig-zag); optional int64 histogram accumulated in `hist`."""
+    _contig(img, "img"); _contig(out, "out")
+    F, H, W, C = img.shape
+    t = N.table_arg(table)
+    # NumPy result type of (DCT output) / table: float32 only for float32 images and tables
+    tdt = np.asarray(table).dtype
+    calc = N.F32 if (_dtype_code(img) == N.F32 and tdt == np.float32) else N.F64
+    hp, nb = (0, 0)
+    if hist is not None:
+        _contig(hist, "hist")
+        hp, nb = hist.data_ptr(), hist.numel()
+    N.check(N.lib().ivc_intra_encode_dev(img.data_ptr(), _dtype_code(img), F, H, W, C, N.ptr(t),
+                                         calc, int(bool(zigzag)), out.data_ptr(), hp or None,
+                                         hist_lo, nb, _stream(stream)), "intra_encode")
+
+
+def inter_encode(frames, sr, table, mv, out, zigzag=False, stream=None):
+    """frames [F, H, W] uint8 -> mv [F-1, H/8, W/8] int64 and out [F-1, H/8, W/8, 3, 64]:
+    ME(frames[f-1], frames[f]) (exact SSD) -> MC -> residual -> DCT -> quantize."""
+    for t_, n in ((frames, "frames"), (mv, "mv"), (out, "out")):
+        _contig(t_, n)
+    F, H, W = frames.shape
+    t = N.table_arg(table)
+    N.check(N.lib().ivc_inter_encode_dev(frames.data_ptr(), F, H, W, int(sr), N.ptr(t), N.F64,
+                                         int(bool(zigzag)), mv.data_ptr(), out.data_ptr(),
+                                         _stream(stream)), "inter_encode")
+
+
+def motion_estimate(ref, cur, sr, mv, exact_u8=False, stream=None):
+    """ref/cur [F, H, W] -> mv [F, H/8, W/8] int64 (motion.py:8-58 semantics)."""
+    _contig(ref, "ref"); _contig(cur, "cur"); _contig(mv, "mv")
+    F, H, W = ref.shape
+    N.check(N.lib().ivc_motion_estimate_dev(ref.data_ptr(), cur.data_ptr(), _dtype_code(ref), F,
+                                            H, W, int(sr), N.ME_EXACT_U8 if exact_u8 else N.ME_NUMPY,
+                                            mv.data_ptr(), _stream(stream)), "motion_estimate")
+
+
+def histogram(sym, lo, hist, stream=None):
+    """hist[v - lo] += 1 over the int32 tensor sym (clamped into the end bins)."""
+    _contig(sym, "sym"); _contig(hist, "hist")
+    N.check(N.lib().ivc_histogram_i32_dev(sym.data_ptr(), sym.numel(), int(lo), hist.numel(),
+                                          hist.data_ptr(), _stream(stream)), "histogram")

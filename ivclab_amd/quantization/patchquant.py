@@ -1,0 +1,96 @@
+"""PatchQuant — drop-in for ivclab/quantization/patchquant.py:3-78.
+
+The table is built on the host exactly as the reference builds it (NumPy stack and scale,
+so its dtype follows NumPy's promotion of the scale); quantize / dequantize run in libivc's
+element-wise gfx950 kernels with NumPy's broadcasting against [1, 1, 3, 8, 8], NumPy's
+result dtype for the division / product, round-half-even and the truncating int32 cast.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import _native as N
+
+_LUM = np.asarray([
+    [16, 11, 10, 16, 24, 40, 51, 61],
+    [12, 12, 14, 19, 26, 58, 60, 55],
+    [14, 13, 16, 24, 40, 57, 69, 56],
+    [14, 17, 22, 29, 51, 87, 80, 62],
+    [18, 55, 37, 56, 68, 109, 103, 77],
+    [24, 35, 55, 64, 81, 104, 113, 92],
+    [49, 64, 78, 87, 103, 121, 120, 101],
+    [72, 92, 95, 98, 112, 100, 103, 99]]).astype(np.float32)
+_CHROM = np.asarray([
+    [17, 18, 24, 47, 99, 99, 99, 99],
+    [18, 21, 26, 66, 99, 99, 99, 99],
+    [24, 13, 56, 99, 99, 99, 99, 99],
+    [47, 66, 99, 99, 99, 99, 99, 99]] + [[99] * 8] * 4).astype(np.float32)
+
+
+def _as_blocks(x: np.ndarray, table: np.ndarray):
+    """Broadcast x against table[None, None] ([1,1,3,8,8]) the way NumPy would, returning
+    (contiguous [nblk, C, 64] source, C, output shape)."""
+    out_shape = np.broadcast_shapes(x.shape, (1, 1) + table.shape)
+    if x.shape == (8, 8):
+        return np.ascontiguousarray(x), 1, out_shape
+    if x.ndim >= 3 and x.shape[-2:] == (8, 8) and x.shape[-3] in (1, 3):
+        return np.ascontiguousarray(x), x.shape[-3], out_shape
+    return np.ascontiguousarray(np.broadcast_to(x, out_shape)), 3, out_shape
+
+
+def _kernel_input(x: np.ndarray) -> np.ndarray:
+    if x.dtype == np.bool_:
+        return x.view(np.uint8)
+    if x.dtype == np.float16:
+        return x.astype(np.float32)
+    if x.dtype not in N.DTYPE_CODE:
+        raise TypeError(f"ivclab_amd: unsupported dtype {x.dtype} for PatchQuant")
+    return x
+
+
+class PatchQuant:
+    """An object that handles forward and inverse quantization of a patched image where
+    each pixel of the patch is quantized with different values depending on the given
+    matrices (reference: ivclab/quantization/patchquant.py:3-78)."""
+
+    def __init__(self, quantization_scale=1.0, luminance=None, chrominance=None):
+        self.quantization_scale = quantization_scale
+        self.luminance = luminance
+        self.chrominance = chrominance
+        if self.luminance is None:
+            self.luminance = _LUM.copy()
+        if self.chrominance is None:
+            self.chrominance = _CHROM.copy()
+
+    def get_quantization_table(self):
+        """stack([lum, chrom, chrom]) * scale (patchquant.py:39-42)."""
+        quantization_table = np.stack([self.luminance, self.chrominance, self.chrominance], axis=0)
+        return quantization_table * self.quantization_scale
+
+    def _run(self, x, entry: str, what: str):
+        x = np.asarray(x)
+        table = np.asarray(self.get_quantization_table())
+        if table.shape != (3, 8, 8):
+            raise ValueError(f"{what}: quantization table must be 3 x 8 x 8, got {table.shape}")
+        calc = np.result_type(x.dtype, table.dtype)
+        if calc not in (np.float32, np.float64):
+            raise TypeError(f"ivclab_amd: {what} arithmetic in {calc} is not supported")
+        src, C, out_shape = _as_blocks(x, table)
+        out = np.empty(out_shape, dtype=np.int32)
+        nblk = out.size // 192
+        if nblk == 0:
+            return out
+        src = np.ascontiguousarray(_kernel_input(src))
+        t = N.table_arg(table)
+        fn = getattr(N.lib(), entry)
+        N.check(fn(N.ptr(src), N.DTYPE_CODE[src.dtype], nblk, C, N.ptr(t),
+                   N.DTYPE_CODE[np.dtype(calc)], N.ptr(out)), what)
+        return out
+
+    def quantize(self, patched_img):
+        """round_half_even(patched_img / table) as int32 (patchquant.py:44-60)."""
+        return self._run(patched_img, "ivc_quantize", "PatchQuant.quantize")
+
+    def dequantize(self, quantized_img):
+        """(quantized_img * table) truncated to int32 (patchquant.py:62-78)."""
+        return self._run(quantized_img, "ivc_dequantize", "PatchQuant.dequantize")

@@ -1,0 +1,61 @@
+"""DiscreteCosineTransform — drop-in for ivclab/signal/dct.py:4-46.
+
+Same constructor, attribute and methods; the 2-D DCT-II / DCT-III of every trailing 8x8
+block runs in libivc's gfx950 kernel, which reproduces scipy.fft's pocketfft op sequence
+bit for bit (dtype rules as scipy: float32 -> float32, other real dtypes -> float64).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .. import _native as N
+
+
+def dct2d(a, norm="ortho", inverse=False) -> np.ndarray:
+    """dct (or idct) along axis -1 then axis -2 of every trailing 8x8 block of `a`."""
+    if norm not in N.NORM_CODE:
+        raise ValueError(f'Invalid norm value {norm!r}, should be "backward", "ortho" or "forward"')
+    x = np.asarray(a)
+    if np.iscomplexobj(x):  # scipy transforms the real and imaginary parts separately
+        re = dct2d(x.real, norm, inverse)
+        return re + 1j * dct2d(x.imag, norm, inverse)
+    if x.ndim < 2:
+        raise np.exceptions.AxisError(-2, x.ndim)
+    if x.shape[-1] < 1 or x.shape[-2] < 1:
+        raise ValueError(f"invalid number of data points ({min(x.shape[-2:])}) specified")
+    if x.shape[-2:] != (8, 8):
+        raise NotImplementedError(
+            f"ivclab_amd: DCT is implemented for 8x8 blocks (the codec block size); got {x.shape[-2:]}")
+    if x.dtype == np.float16:
+        x = x.astype(np.float32)          # scipy's _asfarray does the same
+    elif x.dtype == np.bool_:
+        x = x.view(np.uint8)
+    if x.dtype not in N.DTYPE_CODE:
+        raise TypeError(f"ivclab_amd: unsupported dtype {x.dtype} for the DCT")
+    out_dtype = np.float32 if x.dtype == np.float32 else np.float64
+    out = np.empty(x.shape, dtype=out_dtype)
+    nblk = x.size // 64
+    if nblk == 0:
+        return out
+    x = np.ascontiguousarray(x)
+    L = N.lib()
+    N.check(L.ivc_dct8x8(N.ptr(x), N.DTYPE_CODE[x.dtype], nblk, N.ptr(out),
+                         N.DTYPE_CODE[np.dtype(out_dtype)], 1 if inverse else 0,
+                         N.NORM_CODE[norm]), "DiscreteCosineTransform")
+    return out
+
+
+class DiscreteCosineTransform:
+    """A class to implement the forward and inverse transform of the DCT Type II
+    (reference: ivclab/signal/dct.py:4-46)."""
+
+    def __init__(self, norm="ortho"):
+        self.norm = norm
+
+    def transform(self, patched_img: np.ndarray) -> np.ndarray:
+        """DCT-II along the last axis, then the second-to-last (dct.py:12-28)."""
+        return dct2d(patched_img, self.norm, inverse=False)
+
+    def inverse_transform(self, transformed: np.ndarray) -> np.ndarray:
+        """DCT-III along the last axis, then the second-to-last (dct.py:30-46)."""
+        return dct2d(transformed, self.norm, inverse=True)

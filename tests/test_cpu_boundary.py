@@ -1,0 +1,141 @@
+"""CPU-side checks of the boundary: libivc.so loads, exports every symbol include/ivc.h
+declares, the Python mirror keeps the reference's signatures and fails loudly (no CPU
+fallback) when no gfx950 device is present."""
+import inspect
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _build_lib():
+    from ivclab_amd import build
+    return build.build()
+
+
+@pytest.fixture(scope="module")
+def lib():
+    _build_lib()
+    from ivclab_amd import _native as N
+    return N.load_library()
+
+
+def header_symbols():
+    src = open(os.path.join(ROOT, "include", "ivc.h")).read()
+    decl = r"^\s*(?:int|const char\s*\*)\s*(ivc_[a-z0-9_]+)\s*\("
+    return sorted(set(re.findall(decl, src, re.M)))
+
+
+def test_header_symbols_exported(lib):
+    import ivclab_amd._native as N
+    syms = header_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(lib, s), f"libivc.so does not export {s}"
+    assert set(syms) == set(N.EXPORTS), "ctypes signature table out of sync with include/ivc.h"
+
+
+def test_nm_shows_gfx950_code_object(lib):
+    from ivclab_amd import build
+    data = open(build.OUT, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_no_device_fails_loudly(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is visible")
+    from ivclab_amd import _native as N
+    from ivclab_amd.signal import DiscreteCosineTransform
+    assert lib.ivc_device_count() == 0
+    with pytest.raises(N.IvcError, match="no CPU fallback"):
+        DiscreteCosineTransform().transform(np.zeros((8, 8)))
+
+
+def test_status_mapping(lib):
+    from ivclab_amd import _native as N
+    # a bad dtype code fails argument validation before any device work
+    rc = lib.ivc_quantize(None, 99, 1, 1, None, 10, None)
+    assert rc == N.E_DTYPE
+    with pytest.raises(ValueError, match="invalid source dtype"):
+        N.check(rc, "quantize")
+    rc = lib.ivc_motion_estimate(None, None, 10, 1, 12, 16, 4, 0, None)
+    assert rc == N.E_SHAPE
+    assert b"multiples of 8" in lib.ivc_last_error()
+
+
+def test_reference_signatures():
+    """Same constructor parameters and methods as the reference classes."""
+    import ivclab_amd as IA
+    from ivclab_amd.signal.zigzag import zigzag_scan
+    sig = lambda f: list(inspect.signature(f).parameters)  # noqa: E731
+    assert sig(IA.DiscreteCosineTransform.__init__) == ["self", "norm"]
+    assert IA.DiscreteCosineTransform().norm == "ortho"
+    assert sig(IA.PatchQuant.__init__) == ["self", "quantization_scale", "luminance", "chrominance"]
+    q = IA.PatchQuant()
+    assert q.quantization_scale == 1.0 and q.luminance.dtype == np.float32
+    assert sig(IA.MotionCompensator.__init__) == ["self", "search_range"]
+    assert IA.MotionCompensator().search_range == 4
+    assert sig(IA.Patcher.__init__) == ["self", "window_size"]
+    assert sig(zigzag_scan) == ["block"]
+    for cls, meths in ((IA.DiscreteCosineTransform, ["transform", "inverse_transform"]),
+                       (IA.PatchQuant, ["get_quantization_table", "quantize", "dequantize"]),
+                       (IA.ZigZag, ["flatten", "unflatten"]), (IA.Patcher, ["patch", "unpatch"]),
+                       (IA.MotionCompensator, ["compute_motion_vector",
+                                               "reconstruct_with_motion_vector"])):
+        for m in meths:
+            assert callable(getattr(cls, m))
+
+
+def test_host_logic_tables_and_layout(golden):
+    """Host-side pieces that need no device: table construction and patch views."""
+    import ivclab_amd as IA
+    from oracle import ivc_oracle as O
+    q = golden("quant")
+    for i, s in enumerate(q["scales"]):
+        t = IA.PatchQuant(float(s)).get_quantization_table()
+        assert t.dtype == q[f"table_{i}"].dtype and t.tobytes() == q[f"table_{i}"].tobytes()
+    img = q["img3"]
+    assert np.array_equal(IA.Patcher().patch(img), O.patch(img))
+    assert np.array_equal(IA.Patcher().unpatch(IA.Patcher().patch(img)), img)
+    assert np.array_equal(IA.ZigZag().zigzag_order, O.ZZ_ORDER)
+    from ivclab_amd.quantization.patchquant import _as_blocks
+    src, C, shp = _as_blocks(np.zeros((4, 5, 1, 8, 8)), t)
+    assert C == 1 and shp == (4, 5, 3, 8, 8)
+    src, C, shp = _as_blocks(np.zeros((8, 8)), t)
+    assert C == 1 and shp == (1, 1, 3, 8, 8)
+    src, C, shp = _as_blocks(np.zeros((1, 8)), t)
+    assert C == 3 and shp == (1, 1, 3, 8, 8) and src.shape == shp
+    with pytest.raises(ValueError):
+        _as_blocks(np.zeros((2, 8, 8)), t)
+
+
+def test_install_as_ivclab():
+    import sys
+
+    import ivclab_amd as IA
+    IA.install_as_ivclab()
+    try:
+        from ivclab.quantization import PatchQuant
+        from ivclab.signal import DiscreteCosineTransform
+        from ivclab.signal.zigzag import zigzag_scan  # noqa: F401
+        from ivclab.utils import Patcher, ZigZag  # noqa: F401
+        from ivclab.utils.metrics import calc_mse
+        from ivclab.video import MotionCompensator  # noqa: F401
+        assert DiscreteCosineTransform is IA.DiscreteCosineTransform
+        assert PatchQuant is IA.PatchQuant
+        assert calc_mse(np.zeros((2, 2, 3)), np.ones((2, 2, 3))) == 1.0
+    finally:
+        for k in [k for k in sys.modules if k == "ivclab" or k.startswith("ivclab.")]:
+            del sys.modules[k]
+
+
+def test_single_hip_runtime_with_torch(lib):
+    """libivc and torch must share one HIP runtime (two runtimes cannot both own the GPU)."""
+    import torch  # noqa: F401
+    maps = open("/proc/self/maps").read().splitlines()
+    hips = {ln.split()[-1] for ln in maps if "libamdhip64" in ln}
+    assert len(hips) == 1, hips

@@ -1,0 +1,359 @@
+"""Parity of the HIP path (through the C-ABI, via the ivclab-signature classes) with the
+oracle and with the reference's golden vectors.  Bar: bit-exact for every output (float
+DCT outputs included — the kernels reproduce pocketfft's op order exactly, which is
+stricter than the 1e-5 relative tolerance north_star allows for float DCT)."""
+import numpy as np
+import pytest
+
+from oracle import c_motion_compensate, c_motion_vectors
+from oracle import ivc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+IA = pytest.importorskip("ivclab_amd")
+from ivclab_amd import MotionCompensator, Patcher, PatchQuant, ZigZag  # noqa: E402
+from ivclab_amd.signal import DiscreteCosineTransform  # noqa: E402
+from ivclab_amd.signal.zigzag import zigzag_scan  # noqa: E402
+
+DCT = DiscreteCosineTransform()
+ALL_DTYPES = [np.uint8, np.int8, np.uint16, np.int16, np.uint32, np.int32, np.uint64,
+              np.int64, np.float32, np.float64]
+
+
+def bits_equal(a, b):
+    a, b = np.asarray(a), np.asarray(b)
+    return a.dtype == b.dtype and a.shape == b.shape and a.tobytes() == b.tobytes()
+
+
+def assert_bits(a, b, what=""):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.dtype == b.dtype, f"{what}: dtype {a.dtype} != {b.dtype}"
+    assert a.shape == b.shape, f"{what}: shape {a.shape} != {b.shape}"
+    if a.tobytes() != b.tobytes():
+        bad = np.flatnonzero(a.reshape(-1).view(np.uint8) != b.reshape(-1).view(np.uint8))
+        raise AssertionError(f"{what}: {bad.size} differing bytes, first at byte {bad[0]}")
+
+
+def rand_array(rng, dtype, shape):
+    dtype = np.dtype(dtype)
+    if dtype.kind == "f":
+        return (rng.normal(0, 80, shape)).astype(dtype)
+    info = np.iinfo(dtype)
+    lo, hi = max(info.min, -300), min(info.max, 300)
+    return rng.integers(lo, hi + 1, shape).astype(dtype)
+
+
+# ------------------------------------------------------------------------ DCT ----------
+def test_dct_golden(golden):
+    d = golden("dct")
+    assert_bits(DCT.transform(d["x_u8"]), d["dct_u8"], "dct u8")
+    assert_bits(DCT.transform(d["x_f64"]), d["dct_f64"], "dct f64")
+    assert_bits(DCT.inverse_transform(d["x_f64"]), d["idct_f64"], "idct f64")
+    assert_bits(DCT.transform(d["x_f32"]), d["dct_f32"], "dct f32")
+    assert_bits(DCT.inverse_transform(d["x_f32"]), d["idct_f32"], "idct f32")
+    assert_bits(DCT.inverse_transform(d["x_i32"]), d["idct_i32"], "idct i32")
+    assert_bits(DCT.transform(d["x_i16"]), d["dct_i16"], "dct i16")
+    for norm in ("backward", "forward"):
+        D2 = DiscreteCosineTransform(norm=norm)
+        assert_bits(D2.transform(d["x_f64"][:64]), d[f"dct_f64_{norm}"], norm)
+        assert_bits(D2.inverse_transform(d["x_f64"][:64]), d[f"idct_f64_{norm}"], norm)
+    assert_bits(DCT.transform(Patcher().patch(d["x_img"])), d["dct_img"], "patched view")
+
+
+@pytest.mark.parametrize("dtype", ALL_DTYPES + [np.float16, np.bool_])
+def test_dct_dtypes_vs_oracle(dtype):
+    rng = np.random.default_rng(11)
+    if dtype == np.bool_:
+        x = rng.integers(0, 2, (3, 5, 2, 8, 8)).astype(bool)
+    else:
+        x = rand_array(rng, dtype, (3, 5, 2, 8, 8))
+    assert_bits(DCT.transform(x), O.dct_transform(x), f"dct {dtype}")
+    assert_bits(DCT.inverse_transform(x), O.dct_inverse(x), f"idct {dtype}")
+
+
+def test_dct_shapes_and_errors():
+    rng = np.random.default_rng(3)
+    b = rng.integers(0, 256, (8, 8)).astype(np.uint8)
+    assert_bits(DCT.transform(b), O.dct_transform(b), "bare block")
+    b3 = rng.normal(size=(3, 8, 8)).astype(np.float32)
+    assert_bits(DCT.transform(b3), O.dct_transform(b3), "(3,8,8) float32")
+    e = np.zeros((0, 4, 8, 8))
+    assert DCT.transform(e).shape == (0, 4, 8, 8)
+    nc = rng.normal(size=(4, 8, 8, 3)).transpose(0, 3, 1, 2)  # non-contiguous
+    assert_bits(DCT.transform(nc), O.dct_transform(nc), "non-contiguous")
+    c = rng.normal(size=(2, 8, 8)) + 1j * rng.normal(size=(2, 8, 8))
+    assert np.array_equal(DCT.transform(c), O.dct_transform(c))
+    with pytest.raises(ValueError):
+        DiscreteCosineTransform(norm="bogus").transform(b)
+    with pytest.raises(NotImplementedError):
+        DCT.transform(np.zeros((16, 16)))
+    with pytest.raises(ValueError):
+        DCT.transform(np.zeros(8))
+
+
+def test_dct_large_u8_roundtrip_property():
+    """Full 4K luma frame: bit-exact vs the oracle, and IDCT(DCT(x)) ~= x."""
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (2160, 3840, 1), dtype=np.uint8)
+    p = Patcher().patch(img)
+    y = DCT.transform(p)
+    assert_bits(y, O.dct_transform(p), "4K dct")
+    assert np.allclose(DCT.inverse_transform(y), p, atol=1e-9)
+
+
+# ------------------------------------------------------------------------ quantisation -
+def test_quant_golden(golden):
+    q = golden("quant")
+    d1 = DCT.transform(Patcher().patch(q["img1"]))
+    d3 = DCT.transform(Patcher().patch(q["img3"]))
+    for i, s in enumerate(q["scales"]):
+        Q = PatchQuant(quantization_scale=float(s))
+        assert_bits(Q.get_quantization_table(), q[f"table_{i}"], "table")
+        assert_bits(Q.quantize(d1), q[f"q1_{i}"], f"q1 scale {s}")
+        assert_bits(Q.quantize(d3), q[f"q3_{i}"], f"q3 scale {s}")
+        assert_bits(Q.dequantize(q[f"q1_{i}"]), q[f"dq1_{i}"], f"dq1 scale {s}")
+        assert_bits(Q.dequantize(q[f"q3_{i}"]), q[f"dq3_{i}"], f"dq3 scale {s}")
+        assert_bits(DCT.inverse_transform(q[f"dq3_{i}"]), q[f"idq3_{i}"], f"idq3 scale {s}")
+    Q1 = PatchQuant(1.0)
+    assert_bits(Q1.quantize(Patcher().patch(q["img3"])), q["raw_q3"], "raw pixels")
+    assert_bits(Q1.dequantize(q["raw_q3"]), q["raw_dq3"], "raw dequant")
+    assert_bits(Q1.quantize(q["f32_dct3"]), q["f32_q3"], "float32 dct")
+    assert_bits(Q1.quantize(q["blk88"]), q["blk88_q"], "(8,8)")
+    assert_bits(Q1.quantize(q["blk388"]), q["blk388_q"], "(3,8,8)")
+    assert_bits(Q1.quantize(q["ties_in"]), q["ties_q"], "ties")
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.uint8, np.int16, np.int32,
+                                   np.int64, np.uint64, np.float16, np.bool_])
+@pytest.mark.parametrize("scale", [1.0, 0.07, 2.5])
+def test_quant_dequant_dtypes_vs_oracle(dtype, scale):
+    rng = np.random.default_rng(int(scale * 100))
+    shape = (4, 6, 1, 8, 8) if dtype in (np.uint8, np.int16) else (4, 6, 3, 8, 8)
+    x = rng.integers(0, 2, shape).astype(bool) if dtype == np.bool_ else rand_array(rng, dtype, shape)
+    assert_bits(PatchQuant(scale).quantize(x), O.quantize(x, scale), f"quantize {dtype}")
+    assert_bits(PatchQuant(scale).dequantize(x), O.dequantize(x, scale), f"dequantize {dtype}")
+
+
+def test_quant_scale_dtypes():
+    """A NumPy float64 scale makes a float64 table (NumPy 2 promotion) — follow it."""
+    rng = np.random.default_rng(9)
+    x = rng.normal(0, 300, (2, 2, 3, 8, 8)).astype(np.float32)
+    for s in (np.float64(0.3), np.float32(0.3), 3):
+        Q = PatchQuant(s)
+        ref = np.round(x / Q.get_quantization_table()[None, None]).astype(np.int32)
+        assert_bits(Q.quantize(x), ref, f"scale {type(s)}")
+        refd = (x * Q.get_quantization_table()[None, None]).astype(np.int32)
+        assert_bits(Q.dequantize(x), refd, f"dequant scale {type(s)}")
+
+
+def test_quant_broadcast_and_errors():
+    Q = PatchQuant(0.5)
+    rng = np.random.default_rng(2)
+    for shape in [(8, 8), (3, 8, 8), (1, 8, 8), (2, 3, 1, 8, 8), (5, 1, 1, 3, 8, 8), (1, 8), (),
+                  (4, 4, 3, 1, 8)]:
+        x = rng.normal(0, 100, shape)
+        assert_bits(Q.quantize(x), O.quantize(x, 0.5), f"broadcast {shape}")
+    with pytest.raises(ValueError):
+        Q.quantize(np.zeros((4, 4, 2, 8, 8)))
+    x = np.array([np.nan, np.inf, -np.inf, 1e12, -1e12, 0.5 * 16, 1.5 * 16, 2.5 * 16] * 8)
+    x = x.reshape(1, 1, 1, 8, 8)
+    assert_bits(Q.quantize(x), O.quantize(x, 0.5), "non-finite / out of range")
+    assert_bits(Q.dequantize(np.full((1, 1, 3, 8, 8), 2**30, np.int32)),
+                O.dequantize(np.full((1, 1, 3, 8, 8), 2**30, np.int32), 0.5), "dequant overflow")
+
+
+# ------------------------------------------------------------------------ zig-zag ------
+def test_zigzag_golden(golden):
+    z = golden("zigzag")
+    Z = ZigZag()
+    assert np.array_equal(Z.zigzag_order, z["order"])
+    assert_bits(Z.flatten(z["x5"]), z["flat"], "flatten")
+    assert_bits(Z.unflatten(z["flat"]), z["unflat"], "unflatten")
+    assert_bits(Z.flatten(z["x5_f64"]), z["flat_f64"], "flatten f64")
+    assert_bits(Z.flatten(z["x5_i16"]), z["flat_i16"], "flatten i16")
+    assert_bits(zigzag_scan(z["blk"]), z["scan"], "zigzag_scan")
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.int32, np.float64, np.complex64])
+def test_zigzag_dtypes_and_shapes(dtype):
+    rng = np.random.default_rng(4)
+    x = rng.integers(-100, 100, (3, 4, 2, 8, 8)).astype(dtype)
+    Z = ZigZag()
+    f = Z.flatten(x)
+    assert_bits(f, O.zigzag_flatten(x), f"flatten {dtype}")
+    assert_bits(Z.unflatten(f), x, f"roundtrip {dtype}")
+    wide = rng.integers(-100, 100, (2, 2, 1, 70)).astype(dtype)   # rows wider than 64
+    assert_bits(Z.unflatten(wide), O.zigzag_unflatten(wide), "unflatten wide rows")
+    assert_bits(Z.flatten(x.reshape(3, 4, 2, 4, 16)), O.zigzag_flatten(x.reshape(3, 4, 2, 4, 16)), "4x16")
+    assert Z.flatten(np.zeros((0, 2, 3, 8, 8), dtype)).shape == (0, 2, 3, 64)
+    with pytest.raises(AssertionError):
+        zigzag_scan(np.zeros((4, 4)))
+
+
+# ------------------------------------------------------------------------ motion -------
+ME_CASES = ["shift_f64_sr4", "shift_f64_sr16", "flat_sr4", "nonint_f64_sr4", "f32_sr4",
+            "u8mod_sr4", "u8mod_sr7", "i16_sr4", "i32_sr3", "periodic_f64_sr8",
+            "periodic_f32_sr8", "periodic2_f64_sr5"]
+
+
+@pytest.mark.parametrize("case", ME_CASES)
+def test_me_golden(golden, case):
+    m = golden("motion")
+    ref, cur, sr = m[f"{case}_ref"], m[f"{case}_cur"], int(m[f"{case}_sr"])
+    mv = MotionCompensator(sr).compute_motion_vector(ref, cur)
+    assert_bits(mv, m[f"{case}_mv"], case)
+
+
+@pytest.mark.parametrize("dtype", ALL_DTYPES)
+def test_me_dtypes_vs_c_oracle(dtype):
+    rng = np.random.default_rng(21)
+    base = rand_array(rng, dtype, (80, 96))
+    cur = np.roll(base, (2, -3), axis=(0, 1))
+    cur[::7] = rand_array(rng, dtype, cur[::7].shape)
+    for sr in (0, 3, 9):
+        mv = MotionCompensator(sr).compute_motion_vector(base, cur)
+        assert_bits(mv, c_motion_vectors(base, cur, sr), f"{dtype} sr={sr}")
+
+
+def test_me_large_search_vs_c_oracle():
+    rng = np.random.default_rng(8)
+    a = rng.normal(128, 50, (144, 176))                    # QCIF, non-integer float64
+    b = np.roll(a, (5, -7), axis=(0, 1)) + rng.normal(0, 0.5, a.shape)
+    for sr in (16, 23):
+        assert_bits(MotionCompensator(sr).compute_motion_vector(a, b), c_motion_vectors(a, b, sr),
+                    f"sr={sr}")
+
+
+def test_me_exact_u8_mode_and_mixed_dtypes():
+    import ivclab_amd._native as N
+    rng = np.random.default_rng(12)
+    a = rng.integers(0, 256, (64, 80), dtype=np.uint8)
+    b = np.roll(a, (-4, 6), axis=(0, 1))
+    want = O.motion_vectors(a.astype(np.float64), b.astype(np.float64), 8)
+    mv = np.empty((8, 10, 1), np.int64)
+    N.check(N.lib().ivc_motion_estimate(N.ptr(a), N.ptr(b), 1, 1, 64, 80, 8, N.ME_EXACT_U8, N.ptr(mv)))
+    assert_bits(mv, want, "exact-u8 mode")
+    assert_bits(MotionCompensator(8).compute_motion_vector(a.astype(np.float64), b), want, "f64 vs u8")
+
+
+def test_me_errors():
+    M = MotionCompensator(4)
+    with pytest.raises(ValueError):
+        M.compute_motion_vector(np.zeros((12, 16)), np.zeros((12, 16)))
+    with pytest.raises(TypeError):
+        M.compute_motion_vector(np.zeros((8, 8), bool), np.zeros((8, 8), bool))
+
+
+def test_mc_golden(golden):
+    m = golden("motion")
+    M = MotionCompensator(4)
+    assert_bits(M.reconstruct_with_motion_vector(m["mc_ref1"], m["mc_mv"]), m["mc_out1"], "mc f64")
+    assert_bits(M.reconstruct_with_motion_vector(m["mc_ref3"], m["mc_mv"]), m["mc_out3"], "mc u8x3")
+
+
+@pytest.mark.parametrize("dtype", [np.uint8, np.int16, np.float32, np.float64])
+def test_mc_random_vs_c_oracle(dtype):
+    rng = np.random.default_rng(30)
+    sr = 5
+    ref = rand_array(rng, dtype, (48, 64, 2))
+    mv = rng.integers(-20, (2 * sr + 1) ** 2 + 20, (6, 8, 1))   # includes out-of-range indices
+    got = MotionCompensator(sr).reconstruct_with_motion_vector(ref, mv)
+    assert_bits(got, c_motion_compensate(ref, mv[..., 0], sr), f"mc {dtype}")
+    assert_bits(got, O.motion_compensate(ref, mv, sr), f"mc {dtype} (python)")
+
+
+# ------------------------------------------------------------------------ fused paths --
+def _native():
+    import ivclab_amd._native as N
+    return N, N.lib()
+
+
+@pytest.mark.parametrize("C", [1, 3])
+@pytest.mark.parametrize("zz", [0, 1])
+def test_intra_encode_golden(golden, C, zz):
+    N, L = _native()
+    p = golden("intra")
+    img = np.ascontiguousarray(p[f"img{C}"])
+    H, W, _ = img.shape
+    t = N.table_arg(PatchQuant(0.5).get_quantization_table())
+    out = np.empty((H // 8, W // 8, 3, 64), np.int32)
+    N.check(L.ivc_intra_encode(N.ptr(img), 1, 1, H, W, C, N.ptr(t), N.F64, zz, N.ptr(out)))
+    want = p[f"zz{C}"] if zz else p[f"q{C}"].reshape(H // 8, W // 8, 3, 64)
+    assert_bits(out, want, f"intra C={C} zz={zz}")
+    rec = np.empty((H // 8 * W // 8, 3, 64), np.float64)
+    N.check(L.ivc_intra_decode(N.ptr(p[f"zz{C}"]), (H // 8) * (W // 8), N.ptr(t), N.F64, 1, N.ptr(rec)))
+    assert_bits(rec.reshape(H // 8, W // 8, 3, 8, 8), p[f"rec{C}"], "intra decode")
+
+
+@pytest.mark.parametrize("scale", [1.0, 0.5, 0.15, 2.0, 0.07, 0.013])
+@pytest.mark.parametrize("dtype", [np.uint8, np.float32, np.float64])
+def test_intra_encode_vs_oracle(scale, dtype):
+    N, L = _native()
+    rng = np.random.default_rng(int(scale * 1000) + 1)
+    F, H, W, C = 2, 72, 264, (1 if dtype == np.uint8 else 3)  # w = 33 blocks: ragged tile
+    if dtype == np.uint8:
+        img = rng.integers(0, 256, (F, H, W, C), dtype=np.uint8)
+        img[:, :16] = img[:, :1, :1]                          # flat region: DC ties
+    else:
+        img = rng.normal(128, 60, (F, H, W, C)).astype(dtype)
+    table = PatchQuant(scale).get_quantization_table()
+    t = N.table_arg(table)
+    calc = N.F32 if (dtype == np.float32 and table.dtype == np.float32) else N.F64
+    out = np.empty((F, H // 8, W // 8, 3, 64), np.int32)
+    N.check(L.ivc_intra_encode(N.ptr(img), N.DTYPE_CODE[np.dtype(dtype)], F, H, W, C, N.ptr(t),
+                               calc, 1, N.ptr(out)))
+    for f in range(F):
+        assert_bits(out[f], O.intra_encode(img[f], scale, zigzag=True), f"frame {f}")
+
+
+def test_intra_encode_4k_full_frame():
+    """One full cfg3 frame (3840x2160 luma) bit-exact against the oracle."""
+    N, L = _native()
+    rng = np.random.default_rng(2160)
+    img = rng.integers(0, 256, (1, 2160, 3840, 1), dtype=np.uint8)
+    img[0, 1000:1200] = 77
+    t = N.table_arg(PatchQuant(1.0).get_quantization_table())
+    out = np.empty((1, 270, 480, 3, 64), np.int32)
+    N.check(L.ivc_intra_encode(N.ptr(img), 1, 1, 2160, 3840, 1, N.ptr(t), N.F64, 0, N.ptr(out)))
+    want = O.intra_encode(img[0], 1.0).reshape(270, 480, 3, 64)
+    assert_bits(out[0], want, "4K intra")
+
+
+def test_histogram_vs_oracle():
+    N, L = _native()
+    rng = np.random.default_rng(1)
+    sym = rng.integers(-3000, 3000, 1 << 20).astype(np.int32)
+    sym[::3] = 0
+    for lo, nb in ((-2048, 4096), (-40000, 70000)):
+        h = np.zeros(nb, np.int64)
+        N.check(L.ivc_histogram_i32(N.ptr(sym), sym.size, lo, nb, N.ptr(h)))
+        assert np.array_equal(h, O.histogram(sym, lo, nb))
+
+
+# ------------------------------------------------------------------------ device API ---
+def test_device_api_intra_and_inter():
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(77)
+    F, H, W, sr = 4, 64, 96, 7
+    base = rng.integers(0, 256, (H + 32, W + 32), dtype=np.uint8)
+    frames = np.stack([base[(f % 3):(f % 3) + H, (2 * f % 5):(2 * f % 5) + W] for f in range(F)])
+    frames[2, 10:20, 30:50] = rng.integers(0, 256, (10, 20))
+    dev = torch.device("cuda:0")
+    tf = torch.from_numpy(frames).to(dev)
+    table = PatchQuant(1.0).get_quantization_table()
+    mv = torch.empty((F - 1, H // 8, W // 8), dtype=torch.int64, device=dev)
+    out = torch.empty((F - 1, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+    D.inter_encode(tf, sr, table, mv, out)
+    qi = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+    hist = torch.zeros(8192, dtype=torch.int64, device=dev)
+    D.intra_encode(tf[..., None].contiguous(), table, qi, zigzag=True, hist=hist, hist_lo=-4096)
+    torch.cuda.synchronize()
+    mv, out, qi, hist = mv.cpu().numpy(), out.cpu().numpy(), qi.cpu().numpy(), hist.cpu().numpy()
+    for f in range(1, F):
+        wmv, wq = O.inter_encode(frames[f - 1], frames[f], sr, 1.0)
+        assert_bits(mv[f - 1], wmv[..., 0].astype(np.int64), f"inter mv {f}")
+        assert_bits(out[f - 1], wq.reshape(H // 8, W // 8, 3, 64), f"inter q {f}")
+    for f in range(F):
+        assert_bits(qi[f], O.intra_encode(frames[f][..., None], 1.0, zigzag=True), f"intra {f}")
+    assert np.array_equal(hist, O.histogram(qi, -4096, 8192))
