@@ -10,10 +10,8 @@ namespace ivc {
 
 // quantisation table as kernel argument (by value: no per-call upload on the stream)
 //   q[p*64 + i*8 + k]  : table value in the calc dtype (exactly representable)
-//   rq[...]            : fused kernels only: s_i * s_k * RN(1/q) (see ivc_math.h)
 struct QTab {
   double q[192];
-  double rq[192];
 };
 
 // error raised by a launcher; turned into a status + message by the C-ABI layer
@@ -53,7 +51,5 @@ hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t
                                  int sr, const int64_t* mv, const QTab& t, int zigzag,
                                  int32_t* out, hipStream_t s);
 
-// fill t.rq for the fused kernels' factored DCT (host side)
-void qtab_prepare_fused(QTab& t);
 
 }  // namespace ivc

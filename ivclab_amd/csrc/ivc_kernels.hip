@@ -12,6 +12,9 @@
 // through LDS -> column pass (thread now owns column r) -> results staged in LDS -> the
 // workgroup writes its contiguous output span with 16-byte stores.  HBM traffic per unit
 // is one read of the input and one write of the output.
+#include <mutex>
+#include <unordered_map>
+
 #include "ivc_internal.h"
 #include "ivc_math.h"
 
@@ -300,178 +303,487 @@ hipError_t launch_zigzag(const void* src, int64_t nrow, int64_t stride, int esiz
 // IEEE division taken only when the product lies within 2^-30 of a rounding boundary
 // (proof in DESIGN.md §Quantisation).  Output planes: C = 1 -> (lum, chrom, chrom) from one
 // DCT (patchquant.py:59 broadcast), computed once for the identical chroma planes.
+//
+// Wave-independent schedule: a wave owns tiles of 8 horizontally adjacent blocks (lane =
+// 8*b + r: block b, row r, later column r) and a private LDS region (transpose image +
+// output staging), so a tile needs no workgroup barrier.  The tile index is made provably
+// wave-uniform (readfirstlane) so its decode and the buffer descriptors live in SGPRs.
+// Every global access is an unconditional buffer op whose descriptor range drops the lanes
+// of a ragged tile / the prefetch past the last tile: with no conditional memory ops the
+// compiler can count vmcnt exactly, so the next tile's prefetched row is waited for
+// without waiting for the previous tile's stores.  LDS layouts: transpose image [b][k][r]
+// with block pitch 72 and k pitch 9 (conflict-free b64 writes and reads), output staging
+// with block pitch 200 int32; each tile leaves as 6 x 1 KiB buffer_store_dwordx4.
 // ======================================================================================
 enum { SRC_IMAGE = 0, SRC_INTER = 1 };
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 struct FusedArgs {
   const void* img;       // SRC_IMAGE: [F][H][W][C];  SRC_INTER: u8 frames [F+1][H][W]
   const int64_t* mv;     // SRC_INTER: [F][h][w]
   int32_t* out;          // [F][h][w][3][64]
-  int64_t nframes;       // number of output frames F
-  int H, W, h, w, tpr;   // tpr = tiles (of 32 blocks) per block row
+  uint32_t nframes;      // number of output frames F
+  int H, W, h, w, tpr;   // tpr = tiles (of 8 blocks) per block row
   int sr;
   int dup12;             // table planes 1 and 2 identical (always true for PatchQuant tables)
+#ifdef IVC_ABLATION
+  int ablate;            // diagnostic builds only (tools/ablate): bit mask of skipped phases
+#endif
+};
+#ifdef IVC_ABLATION
+#define IVC_SKIP(a, bit) (((a).ablate & (bit)) != 0)
+#else
+#define IVC_SKIP(a, bit) false
+#endif
+// cache-policy bits of the streamed output stores / input loads (diagnostic builds may
+// override them with -D to compare policies)
+#ifndef IVC_STORE_AUX
+#define IVC_STORE_AUX 0
+#endif
+#ifndef IVC_LOAD_AUX
+#define IVC_LOAD_AUX 0
+#endif
+#ifndef IVC_WIDE_NG
+#define IVC_WIDE_NG 2    // u8 luma: 8 rows x 128 bytes per wave load (whole cache lines)
+#endif
+
+constexpr int XS_PITCH = 72;   // T elements per block in the transpose image
+constexpr int OS_PITCH = 200;  // int32 per block in the output staging (192 + 8 pad)
+constexpr int OOB = 0x40000000;  // buffer offset beyond every descriptor range used here
+
+template <typename T, int C>
+struct WaveLds {
+  static constexpr int XS = 8 * XS_PITCH * (int)sizeof(T);
+  static constexpr int OS = 8 * OS_PITCH * 4;
+  static constexpr int BYTES = C == 1 ? (XS > OS ? XS : OS) : XS + OS;  // C = 1 aliases them
 };
 
-template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC>
-__global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) {
-  constexpr int XS_BYTES = 32 * 72 * (int)sizeof(T);
-  constexpr int OS_BYTES = 32 * 192 * 4;
-  // C == 1: the output staging aliases the transpose buffer (disjoint in time)
-  constexpr int LDS_BYTES = C == 1 ? (XS_BYTES > OS_BYTES ? XS_BYTES : OS_BYTES)
-                                   : XS_BYTES + OS_BYTES;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[LDS_BYTES];
-  __shared__ D sq[192];
-  __shared__ double srq[FAST ? 192 : 1];
-  T* xs = reinterpret_cast<T*>(lds);
-  int32_t* os = reinterpret_cast<int32_t*>(lds + (C == 1 ? 0 : XS_BYTES));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
 
-  const int tid = threadIdx.x, u = tid >> 3, r = tid & 7;
-  for (int i = tid; i < 192; i += 256) {
-    sq[i] = (D)t.q[i];
-    if constexpr (FAST) srq[i] = t.rq[i];
+// A group = 8 horizontally adjacent blocks of one block row (one wave-step of compute and
+// one 6 KiB store); a load tile = NG consecutive groups, whose 8 image rows the wave loads
+// at once.  tpr counts load tiles per block row.
+struct GroupLoc {
+  uint32_t f;
+  int bi, bj0, nb;
+};
+
+template <int NG>
+__device__ __forceinline__ GroupLoc group_loc(const FusedArgs& a, uint32_t lt, int g) {
+  const uint32_t tpf = (uint32_t)(a.h * a.tpr);
+  GroupLoc L;
+  L.f = lt / tpf;
+  const uint32_t rem = lt - L.f * tpf;
+  L.bi = (int)(rem / (uint32_t)a.tpr);
+  L.bj0 = ((int)(rem - (uint32_t)L.bi * a.tpr) * NG + g) * 8;
+  const int left = a.w - L.bj0;
+  L.nb = left < 0 ? 0 : (left < 8 ? left : 8);
+  return L;
+}
+
+// One lane's input row(s) as raw 32-bit words (u8 C = 1: 2 words); unpacked at use.
+template <typename TI, int C, int SRC>
+struct RowReg {
+  static constexpr int NW = SRC == SRC_INTER ? 4 : (8 * C * (int)sizeof(TI)) / 4;
+  uint32_t w[NW];
+  __device__ __forceinline__ TI get(int idx) const {
+    if constexpr (sizeof(TI) == 1) {
+      return (TI)((w[idx >> 2] >> (8 * (idx & 3))) & 0xffu);
+    } else if constexpr (sizeof(TI) == 2) {
+      return (TI)((w[idx >> 1] >> (16 * (idx & 1))) & 0xffffu);
+    } else if constexpr (sizeof(TI) == 4) {
+      return __builtin_bit_cast(TI, w[idx]);
+    } else {
+      const uint64_t u = (uint64_t)w[2 * idx] | ((uint64_t)w[2 * idx + 1] << 32);
+      return __builtin_bit_cast(TI, u);
+    }
   }
-  __syncthreads();
+};
 
-  const int64_t tiles_per_frame = (int64_t)a.h * a.tpr;
-  const int64_t ntiles = a.nframes * tiles_per_frame;
+template <int NW, int AUX>
+__device__ __forceinline__ void buffer_words(__amdgpu_buffer_rsrc_t rs, int off, uint32_t* w) {
+  if constexpr (NW % 4 == 0) {
+#pragma unroll
+    for (int j = 0; j < NW / 4; ++j) {
+      const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16 * j, 0, AUX);
+      w[4 * j] = x.x; w[4 * j + 1] = x.y; w[4 * j + 2] = x.z; w[4 * j + 3] = x.w;
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NW / 2; ++j) {
+      const u32x2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 8 * j, 0, AUX);
+      w[2 * j] = x.x; w[2 * j + 1] = x.y;
+    }
+  }
+}
+
+// Raw input of load tile `lt`.
+//  NG == 1: lane (b, r) holds row r of block b (8*C elements).
+//  NG >= 2 (u8, C = 1): the wave reads 8 rows x 64*NG bytes with one 16-byte load per lane
+//  per 128 bytes (lane L: row L/8, bytes 16*(L%8) of each 128-byte column), i.e. whole
+//  cache lines per row; group_row() redistributes them to the (b, r) layout.
+template <typename TI, int C, int NG>
+struct TileRaw {
+  static constexpr int NW = NG == 1 ? RowReg<TI, C, SRC_IMAGE>::NW : 2 * NG;
+  uint32_t w[NW];
+};
+
+template <typename TI, int C, int NG>
+__device__ __forceinline__ void load_tile(const FusedArgs& a, uint32_t lt, bool exists, int lane,
+                                          TileRaw<TI, C, NG>& t) {
+  const GroupLoc L = group_loc<NG>(a, exists ? lt : 0u, 0);
+  const int64_t base = (((int64_t)L.f * a.H + 8 * L.bi) * a.W + 8 * L.bj0) * C;
+  const uint32_t bytes = exists ? (uint32_t)(8 * a.W * C * (int)sizeof(TI)) : 0u;
+  const __amdgpu_buffer_rsrc_t rs = make_rsrc(reinterpret_cast<const TI*>(a.img) + base, bytes);
+  const int b = lane >> 3, r = lane & 7;
+  if constexpr (NG == 1) {
+    const int off = b < L.nb ? (r * a.W * C + 8 * b * C) * (int)sizeof(TI) : OOB;
+    buffer_words<TileRaw<TI, C, NG>::NW, IVC_LOAD_AUX>(rs, off, t.w);
+  } else {
+    static_assert(sizeof(TI) == 1 && C == 1, "wide tiles are the u8 luma path");
+#pragma unroll
+    for (int j = 0; j < NG / 2; ++j) {
+      const int col = 128 * j + 16 * r;                 // byte column inside the tile
+      const int off = L.bj0 * 8 + col < a.W ? b * a.W + col : OOB;
+      const u32x4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, IVC_LOAD_AUX);
+      t.w[4 * j] = x.x; t.w[4 * j + 1] = x.y; t.w[4 * j + 2] = x.z; t.w[4 * j + 3] = x.w;
+    }
+  }
+}
+
+// Row r of block 8g + b for lane (b, r) from a wide tile: it sits in lane 8r + 4(g%2) + b/2,
+// 16-byte column g/2, half b%2 — four ds_bpermute per group.
+template <typename TI, int C, int NG>
+__device__ __forceinline__ void group_row(const TileRaw<TI, C, NG>& t, int g, int lane,
+                                          RowReg<TI, C, SRC_IMAGE>& v) {
+  if constexpr (NG == 1) {
+#pragma unroll
+    for (int k = 0; k < TileRaw<TI, C, NG>::NW; ++k) v.w[k] = t.w[k];
+  } else {
+    const int b = lane >> 3, r = lane & 7;
+    const int j = g >> 1;
+    const int src = (8 * r + 4 * (g & 1) + (b >> 1)) * 4;
+    const uint32_t p0 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)t.w[4 * j]);
+    const uint32_t p1 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)t.w[4 * j + 1]);
+    const uint32_t p2 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)t.w[4 * j + 2]);
+    const uint32_t p3 = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)t.w[4 * j + 3]);
+    v.w[0] = (b & 1) ? p2 : p0;
+    v.w[1] = (b & 1) ? p3 : p1;
+  }
+}
+
+// Residual rows of group `lt` (inter path, NG = 1): cur - block-copy prediction.
+__device__ __forceinline__ void gather_inter(const FusedArgs& a, uint32_t lt, int b, int r,
+                                             RowReg<int16_t, 1, SRC_INTER>& v) {
+  const GroupLoc L = group_loc<1>(a, lt, 0);
+  const uint8_t* fr = reinterpret_cast<const uint8_t*>(a.img);
+  const int64_t HW = (int64_t)a.H * a.W;
+  const __amdgpu_buffer_rsrc_t rmv =
+      make_rsrc(a.mv + ((int64_t)L.f * a.h + L.bi) * a.w + L.bj0, (uint32_t)L.nb * 8u);
+  const u32x2 mw = __builtin_amdgcn_raw_buffer_load_b64(rmv, b < L.nb ? b * 8 : OOB, 0, 0);
+  const int64_t m = (int64_t)(((uint64_t)mw.y << 32) | mw.x);
+  const __amdgpu_buffer_rsrc_t rcur = make_rsrc(
+      fr + (int64_t)(L.f + 1) * HW + (int64_t)(8 * L.bi) * a.W + 8 * L.bj0, (uint32_t)(8 * a.W));
+  const u32x2 cw = __builtin_amdgcn_raw_buffer_load_b64(rcur, b < L.nb ? r * a.W + 8 * b : OOB, 0, 0);
   const int n = 2 * a.sr + 1;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t f = tile / tiles_per_frame;
-    const int rem = (int)(tile - f * tiles_per_frame);
-    const int bi = rem / a.tpr;
-    const int bj0 = (rem - bi * a.tpr) * 32;
-    const int bj = bj0 + u;
-    const bool ok = bj < a.w;
+  int64_t qd = m / n, rm = m - qd * n;  // Python floor division (motion.py:83-84)
+  if (rm < 0) { rm += n; qd -= 1; }
+  const int dy = (int)qd - a.sr, dx = (int)rm - a.sr;
+  const int ry = 8 * L.bi + dy, rx = 8 * (L.bj0 + b) + dx;
+  // prediction is zero where the displaced block leaves the frame (motion.py:89-92)
+  const bool in = b < L.nb && ry >= 0 && ry + 8 <= a.H && rx >= 0 && rx + 8 <= a.W;
+  const __amdgpu_buffer_rsrc_t rref = make_rsrc(fr + (int64_t)L.f * HW, (uint32_t)HW);
+  const int roff = (ry + r) * a.W + rx;
+  const int o = in ? (roff & ~3) : OOB;
+  const uint32_t q0 = __builtin_amdgcn_raw_buffer_load_b32(rref, o, 0, 0);
+  const uint32_t q1 = __builtin_amdgcn_raw_buffer_load_b32(rref, o + 4, 0, 0);
+  const uint32_t q2 = __builtin_amdgcn_raw_buffer_load_b32(rref, o + 8, 0, 0);
+  const uint32_t sh = (uint32_t)(roff & 3);
+  const uint32_t p0 = __builtin_amdgcn_alignbyte(q1, q0, sh);
+  const uint32_t p1 = __builtin_amdgcn_alignbyte(q2, q1, sh);
+#pragma unroll
+  for (int k = 0; k < 8; k += 2) {
+    const uint32_t cs = k < 4 ? cw.x : cw.y, ps = k < 4 ? p0 : p1;
+    const int d0 = (int)((cs >> (8 * (k & 3))) & 0xffu) - (int)((ps >> (8 * (k & 3))) & 0xffu);
+    const int d1 = (int)((cs >> (8 * ((k + 1) & 3))) & 0xffu) - (int)((ps >> (8 * ((k + 1) & 3))) & 0xffu);
+    v.w[k >> 1] = ((uint32_t)d0 & 0xffffu) | ((uint32_t)d1 << 16);
+  }
+}
 
-    // ---- gather this thread's row of every channel ----------------------------------
-    TI v[8 * C];
-    if (ok) {
-      if constexpr (SRC == SRC_IMAGE) {
-        const TI* p = reinterpret_cast<const TI*>(a.img) +
-                      (((int64_t)f * a.H + 8 * bi + r) * a.W + 8 * bj) * C;
-        if constexpr (C == 1) {
-          alignas(16) TI tmp[8];
-          load8<TI>(p, tmp);
+// The staged group (LDS, block pitch OS_PITCH) leaves as 6 x 1 KiB buffer_store_dwordx4;
+// lanes past a ragged group's edge, or a non-existent group, fall outside the descriptor.
+template <int NG>
+__device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* os, int lane,
+                                            uint32_t lt, int g, bool exists) {
+  const GroupLoc L = group_loc<NG>(a, lt, g);
+  const __amdgpu_buffer_rsrc_t ro =
+      make_rsrc(a.out + (((int64_t)L.f * a.h + L.bi) * a.w + L.bj0) * 192,
+                exists ? (uint32_t)L.nb * 768u : 0u);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) v[k] = tmp[k];
-        } else {
+  for (int jj = 0; jj < 6; ++jj) {
+    const int ch = lane + 64 * jj;
+    const int bb = ch / 48;
+    const int4 val = *reinterpret_cast<const int4*>(os + bb * OS_PITCH + (ch - bb * 48) * 4);
+    const u32x4 w4 = {(uint32_t)val.x, (uint32_t)val.y, (uint32_t)val.z, (uint32_t)val.w};
+    __builtin_amdgcn_raw_buffer_store_b128(w4, ro, ch * 16, 0, IVC_STORE_AUX);
+  }
+}
+
+// Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging.
+template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG>
+__device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI, C, SRC>& v,
+                                             T* xs, int32_t* os, const double2* srq, const D* sq,
+                                             int b, int r, uint32_t zp0, uint32_t zp1) {
 #pragma unroll
-          for (int k = 0; k < 8 * C; ++k) v[k] = p[k];
-        }
+  for (int c = 0; c < C; ++c) {
+    // ---- row pass (axis -1): lane owns row r of block b ------------------------------------
+    T x[8];
+    if constexpr (FAST) {
+      int xi[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) xi[k] = (int)v.get(k * C + c);
+      if (IVC_SKIP(a, 1)) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) x[k] = (double)xi[k];
       } else {
-        // residual of the motion-compensated prediction; prediction is zero where the
-        // displaced block leaves the frame (motion.py:89-92)
-        const uint8_t* fr = reinterpret_cast<const uint8_t*>(a.img);
-        const int64_t HW = (int64_t)a.H * a.W;
-        const uint8_t* cur = fr + (f + 1) * HW + (int64_t)(8 * bi + r) * a.W + 8 * bj;
-        const int64_t m = a.mv[(f * a.h + bi) * a.w + bj];
-        int64_t qd = m / n, rm = m - qd * n;
-        if (rm < 0) { rm += n; qd -= 1; }
-        const int dy = (int)qd - a.sr, dx = (int)rm - a.sr;
-        const int ry = 8 * bi + dy, rx = 8 * bj + dx;
-        const bool in = ry >= 0 && ry + 8 <= a.H && rx >= 0 && rx + 8 <= a.W;
-        alignas(8) uint8_t cb[8];
-        *reinterpret_cast<uint2*>(cb) = *reinterpret_cast<const uint2*>(cur);
-        const uint8_t* ref = fr + f * HW + (int64_t)(ry + r) * a.W + rx;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = (TI)((int)cb[k] - (in ? (int)ref[k] : 0));
+        dct2_row_int(xi, x);
       }
     } else {
 #pragma unroll
-      for (int k = 0; k < 8 * C; ++k) v[k] = TI(0);
+      for (int k = 0; k < 8; ++k) x[k] = (T)v.get(k * C + c);
+      dct2_line<T>(x, T(0.25), true);
     }
-
+    T y[8];
+    if (IVC_SKIP(a, 8)) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      // ---- row pass (axis -1) ----------------------------------------------------------
-      T x[8];
-      if constexpr (FAST) {
-        int xi[8];
+      for (int i = 0; i < 8; ++i) y[i] = x[i];
+    } else {
+      // transpose image [b][k][r], pitch 9: conflict-free b64 writes and reads
 #pragma unroll
-        for (int k = 0; k < 8; ++k) xi[k] = (int)v[k * C + c];
-        dct2_row_int(xi, x);
-      } else {
+      for (int k = 0; k < 8; ++k) xs[b * XS_PITCH + k * 9 + r] = x[k];
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = (T)v[k * C + c];
-        dct2_line<T>(x, T(0.25), true);
-      }
-#pragma unroll
-      for (int k = 0; k < 8; ++k) xs[u * 72 + r * 9 + k] = x[k];
-      __syncthreads();
-      T y[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) y[i] = xs[u * 72 + i * 9 + r];
-      __syncthreads();
-      // ---- column pass (axis -2); thread now owns column k = r -------------------------
-      if constexpr (FAST) {
-        dct2_col_unscaled(y, x);
-      } else {
+      for (int i = 0; i < 8; ++i) y[i] = xs[b * XS_PITCH + r * 9 + i];
+      __builtin_amdgcn_wave_barrier();
+    }
+    // ---- column pass (axis -2): lane now owns column r --------------------------------------
+    if constexpr (FAST) {
+      if (IVC_SKIP(a, 2)) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) x[i] = y[i];
-        dct2_line<T>(x, T(0.25), true);
+      } else {
+        dct2_col_unscaled(y, x);
       }
-      // ---- quantise ----------------------------------------------------------------------
-      const int np = C == 1 ? (a.dup12 ? 2 : 3) : 1;
-      for (int pi = 0; pi < np; ++pi) {
-        const int p = C == 1 ? pi : c;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) x[i] = y[i];
+      dct2_line<T>(x, T(0.25), true);
+    }
+    // ---- quantise ---------------------------------------------------------------------------
+#pragma unroll
+    for (int pi = 0; pi < (C == 1 ? 3 : 1); ++pi) {
+      if (C == 1 && pi == 2 && a.dup12) break;  // plane 2 == plane 1: written with plane 1
+      const int p = C == 1 ? pi : c;
+      int qv[8];
+      if (IVC_SKIP(a, 4)) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) qv[i] = (int)x[i];
+      } else if constexpr (FAST) {
+        bool all_ok = true;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const int j = i * 8 + r;
-          int q;
-          if constexpr (FAST) {
-            const double yq = x[i] * srq[p * 64 + j];
-            const double rr = __builtin_rint(yq);
-            if (__builtin_fabs(yq - rr) < 0.5 - 0x1p-30 && __builtin_fabs(yq) < 0x1p20) {
-              q = (int)rr;
-            } else {
-              const double Y = x[i] * (dct2_scale(i) * dct2_scale(r));
-              q = np_to_i32<double>(__builtin_rint(Y / (double)sq[p * 64 + j]));
-            }
-          } else {
-            q = np_to_i32<D>(rint_t<D>((D)x[i] / sq[p * 64 + j]));
-          }
-          const int pos = ZZ ? c_zz_order[j] : j;
-          os[u * 192 + p * 64 + pos] = q;
-          if (C == 1 && p == 1 && a.dup12) os[u * 192 + 128 + pos] = q;
+          const double2 e = srq[p * 64 + i * 8 + r];
+          const double yq = x[i] * e.x;
+          const double rr = __builtin_rint(yq);
+          bool ok = __builtin_fabs(yq - rr) < e.y;
+          if (CHECKMAG) ok = ok && __builtin_fabs(yq) < 0x1p20;
+          all_ok = all_ok && ok;
+          qv[i] = (int)rr;
         }
+        // exact IEEE division next to a rounding boundary (rare; one wave-uniform test)
+        if (__ballot(!all_ok)) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const double2 e = srq[p * 64 + i * 8 + r];
+            const double yq = x[i] * e.x;
+            const double rr = __builtin_rint(yq);
+            bool ok = __builtin_fabs(yq - rr) < e.y;
+            if (CHECKMAG) ok = ok && __builtin_fabs(yq) < 0x1p20;
+            if (!ok) {
+              const double Y = x[i] * (dct2_scale(i) * dct2_scale(r));
+              qv[i] = np_to_i32<double>(__builtin_rint(Y / (double)sq[p * 64 + i * 8 + r]));
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          qv[i] = np_to_i32<D>(rint_t<D>((D)x[i] / sq[p * 64 + i * 8 + r]));
+      }
+      int32_t* ob = os + b * OS_PITCH + p * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int pos = ZZ ? (int)(((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u) : i * 8 + r;
+        ob[pos] = qv[i];
+        if (C == 1 && pi == 1 && a.dup12) ob[64 + pos] = qv[i];
       }
     }
-    __syncthreads();
-    // ---- contiguous store of the tile's nb x 3 x 64 int32 -------------------------------
-    const int nb = a.w - bj0 < 32 ? a.w - bj0 : 32;
-    int32_t* out = a.out + (((int64_t)f * a.h + bi) * a.w + bj0) * 192;
-    for (int e = tid * 4; e < nb * 192; e += 1024)
-      *reinterpret_cast<int4*>(out + e) = *reinterpret_cast<const int4*>(os + e);
-    __syncthreads();
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
-void qtab_prepare_fused(QTab& t) {
-  for (int p = 0; p < 3; ++p)
-    for (int i = 0; i < 8; ++i)
-      for (int k = 0; k < 8; ++k) {
-        const int j = p * 64 + i * 8 + k;
-        t.rq[j] = (dct2_scale(i) * dct2_scale(k)) * (1.0 / t.q[j]);
+template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
+          int NG>
+__global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) {
+  typedef WaveLds<T, C> L;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
+  __shared__ double2 srq[FAST ? 192 : 1];
+  __shared__ D sq[192];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+  const int b = lane >> 3, r = lane & 7;
+  for (int i = tid; i < 192; i += 256) {
+    sq[i] = (D)t.q[i];
+    // {s_i * s_k * RN(1/q), rounding-boundary threshold}: for a power-of-two q the
+    // reciprocal product IS the exact quotient, so its threshold (> 0.5) never sends it to
+    // the division.  1.0 / q is IEEE-correctly rounded here as on the host.
+    if constexpr (FAST) {
+      const double q = t.q[i];
+      const double rq = (dct2_scale((i >> 3) & 7) * dct2_scale(i & 7)) * (1.0 / q);
+      const uint64_t bits = __builtin_bit_cast(uint64_t, q);
+      const uint32_t ex = (uint32_t)(bits >> 52) & 0x7ffu;
+      const bool pow2 = (bits & 0xfffffffffffffull) == 0 && ex != 0 && ex != 0x7ffu;
+      srq[i] = make_double2(rq, pow2 ? 1.0 : 0.5 - 0x1p-30);
+    }
+  }
+  // zig-zag positions of this lane's column (raster i*8 + r), packed 4 per register
+  uint32_t zp0 = 0, zp1 = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    zp0 |= (uint32_t)(ZZ ? c_zz_order[i * 8 + r] : i * 8 + r) << (8 * i);
+    zp1 |= (uint32_t)(ZZ ? c_zz_order[(i + 4) * 8 + r] : (i + 4) * 8 + r) << (8 * i);
+  }
+  __syncthreads();  // tables only; the loop below never synchronises across waves
+
+  unsigned char* mine = lds + wave * L::BYTES;
+  T* xs = reinterpret_cast<T*>(mine);
+  int32_t* os = reinterpret_cast<int32_t*>(mine + (C == 1 ? 0 : L::XS));
+  const uint32_t nlt = a.nframes * (uint32_t)(a.h * a.tpr);
+  const uint32_t nwaves = gridDim.x * 4u;
+  uint32_t lt = blockIdx.x * 4u + wave;
+
+  // Software pipeline per wave.  Group (lt, g) first issues the stores of the previous group
+  // (staged in LDS); group 0 then issues the prefetch of load tile lt + nwaves; then the
+  // group is transformed.  The prologue issues the same number of (range-dropped) stores, so
+  // every path into a wait for tile lt's rows has the same ops behind that load and the
+  // compiler's vmcnt wait never includes the stores.  Ragged / non-existent groups go
+  // through zero-range descriptors instead of branches.
+  TileRaw<TI, C, NG> raw;
+  if constexpr (SRC == SRC_IMAGE) {
+    load_tile<TI, C, NG>(a, lt, lt < nlt, lane, raw);
+#pragma unroll
+    for (int g = 1; g < NG; ++g) store_group<NG>(a, os, lane, 0u, 0, false);
+  }
+  uint32_t plt = 0;
+  int pg = 0;
+  bool have_prev = false;
+  for (; lt < nlt; lt += nwaves) {
+    TileRaw<TI, C, NG> nraw;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      store_group<NG>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+      RowReg<TI, C, SRC> v;
+      if constexpr (SRC == SRC_IMAGE) {
+        if (g == 0) {
+          const uint32_t nt = lt + nwaves;
+          load_tile<TI, C, NG>(a, nt, nt < nlt && !IVC_SKIP(a, 32), lane, nraw);
+        }
+        group_row<TI, C, NG>(raw, g, lane, v);
+      } else {
+        gather_inter(a, lt, b, r, v);
       }
+      encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+      plt = lt;
+      pg = g;
+      have_prev = true;
+    }
+    if constexpr (SRC == SRC_IMAGE) raw = nraw;
+  }
+  store_group<NG>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+}
+
+
+// Persistent grids: exactly the resident workgroup count (occupancy query, cached per
+// kernel), so no workgroup starts after the first wave of workgroups has drained — a grid
+// above residency runs its surplus as a second, partially occupied wave.
+static std::mutex g_occ_mu;
+static std::unordered_map<const void*, int> g_occ;
+
+template <typename K>
+static unsigned resident_grid(K kernel, int64_t work_groups_needed) {
+  int per_cu = 0;
+  {
+    std::lock_guard<std::mutex> g(g_occ_mu);
+    auto it = g_occ.find((const void*)kernel);
+    if (it != g_occ.end()) {
+      per_cu = it->second;
+    } else {
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess ||
+          per_cu < 1)
+        per_cu = 1;
+      g_occ[(const void*)kernel] = per_cu;
+    }
+  }
+  int64_t g = (int64_t)num_cus() * per_cu;
+  if (work_groups_needed < g) g = work_groups_needed;
+  return (unsigned)(g < 1 ? 1 : g);
+}
+
+// NG: groups of 8 blocks per wave load (wide, whole-cache-line row loads for u8 luma)
+template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CM,
+          int NGW = IVC_WIDE_NG>
+static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s) {
+  constexpr int NG = (sizeof(TI) == 1 && C == 1 && SRC == SRC_IMAGE) ? NGW : 1;
+  FusedArgs a = a_in;
+  a.tpr = (a.w + 8 * NG - 1) / (8 * NG);
+  const int64_t nlt = (int64_t)a.nframes * a.h * a.tpr;
+  auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG>;
+  k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
+}
+
+// The FAST quotient check needs |quotient| < 2^20.  Integer pixels
+// and residuals of u8 frames bound every DCT-II ortho coefficient by 64*255/4 < 4096, so a
+// table with min |q| > 1/256 proves the bound and the per-value magnitude test is dropped.
+static bool needs_magnitude_check(const QTab& t) {
+  for (int i = 0; i < 192; ++i)
+    if (!(__builtin_fabs(t.q[i]) > 1.0 / 256.0) || __builtin_isinf(t.q[i])) return true;
+  return false;
 }
 
 template <typename TI, typename T, typename D, int C, bool FAST, int SRC>
-static void launch_fused_zz(const FusedArgs& a, const QTab& t, int zigzag, unsigned grid,
+static void launch_fused_zz(const FusedArgs& a, const QTab& t, int zigzag, int64_t ntiles,
                             hipStream_t s) {
-  if (zigzag)
-    fused_encode_kernel<TI, T, D, C, FAST, true, SRC><<<grid, 256, 0, s>>>(a, t);
-  else
-    fused_encode_kernel<TI, T, D, C, FAST, false, SRC><<<grid, 256, 0, s>>>(a, t);
+  const bool cm = FAST && needs_magnitude_check(t);
+  if (zigzag) {
+    if (cm) launch_fused_one<TI, T, D, C, FAST, true, SRC, true>(a, t, s);
+    else launch_fused_one<TI, T, D, C, FAST, true, SRC, false>(a, t, s);
+  } else {
+    if (cm) launch_fused_one<TI, T, D, C, FAST, false, SRC, true>(a, t, s);
+    else launch_fused_one<TI, T, D, C, FAST, false, SRC, false>(a, t, s);
+  }
 }
 
 static FusedArgs make_fused_args(const void* img, const int64_t* mv, int32_t* out,
                                  int64_t nframes, int64_t H, int64_t W, int sr,
                                  const QTab& t) {
   FusedArgs a;
-  a.img = img; a.mv = mv; a.out = out; a.nframes = nframes;
+  a.img = img; a.mv = mv; a.out = out; a.nframes = (uint32_t)nframes;
   a.H = (int)H; a.W = (int)W; a.h = (int)(H / 8); a.w = (int)(W / 8);
-  a.tpr = (a.w + 31) / 32;
+  a.tpr = (a.w + 7) / 8;
   a.sr = sr;
   a.dup12 = 1;
   for (int i = 0; i < 64; ++i)
@@ -484,29 +796,28 @@ hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int6
                                hipStream_t s) {
   if (nframes <= 0 || H <= 0 || W <= 0) return hipSuccess;
   if (C != 1 && C != 3) return hipErrorInvalidValue;
-  QTab t = t_in;
-  qtab_prepare_fused(t);
+  const QTab& t = t_in;
   FusedArgs a = make_fused_args(img, nullptr, out, nframes, H, W, 0, t);
   const int64_t ntiles = nframes * (int64_t)a.h * a.tpr;
-  const unsigned grid = grid_for(ntiles, 1, 8);
+  if (ntiles >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit tile indices
   switch (dtype) {
     case IVC_U8:
       if (calc_dtype != IVC_F64) return hipErrorInvalidValue;
-      if (C == 1) launch_fused_zz<uint8_t, double, double, 1, true, SRC_IMAGE>(a, t, zigzag, grid, s);
-      else launch_fused_zz<uint8_t, double, double, 3, true, SRC_IMAGE>(a, t, zigzag, grid, s);
+      if (C == 1) launch_fused_zz<uint8_t, double, double, 1, true, SRC_IMAGE>(a, t, zigzag, ntiles, s);
+      else launch_fused_zz<uint8_t, double, double, 3, true, SRC_IMAGE>(a, t, zigzag, ntiles, s);
       break;
     case IVC_F64:
       if (calc_dtype != IVC_F64) return hipErrorInvalidValue;
-      if (C == 1) launch_fused_zz<double, double, double, 1, false, SRC_IMAGE>(a, t, zigzag, grid, s);
-      else launch_fused_zz<double, double, double, 3, false, SRC_IMAGE>(a, t, zigzag, grid, s);
+      if (C == 1) launch_fused_zz<double, double, double, 1, false, SRC_IMAGE>(a, t, zigzag, ntiles, s);
+      else launch_fused_zz<double, double, double, 3, false, SRC_IMAGE>(a, t, zigzag, ntiles, s);
       break;
     case IVC_F32:
       if (calc_dtype == IVC_F32) {
-        if (C == 1) launch_fused_zz<float, float, float, 1, false, SRC_IMAGE>(a, t, zigzag, grid, s);
-        else launch_fused_zz<float, float, float, 3, false, SRC_IMAGE>(a, t, zigzag, grid, s);
+        if (C == 1) launch_fused_zz<float, float, float, 1, false, SRC_IMAGE>(a, t, zigzag, ntiles, s);
+        else launch_fused_zz<float, float, float, 3, false, SRC_IMAGE>(a, t, zigzag, ntiles, s);
       } else if (calc_dtype == IVC_F64) {
-        if (C == 1) launch_fused_zz<float, float, double, 1, false, SRC_IMAGE>(a, t, zigzag, grid, s);
-        else launch_fused_zz<float, float, double, 3, false, SRC_IMAGE>(a, t, zigzag, grid, s);
+        if (C == 1) launch_fused_zz<float, float, double, 1, false, SRC_IMAGE>(a, t, zigzag, ntiles, s);
+        else launch_fused_zz<float, float, double, 3, false, SRC_IMAGE>(a, t, zigzag, ntiles, s);
       } else {
         return hipErrorInvalidValue;
       }
@@ -521,12 +832,11 @@ hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t
                                  int sr, const int64_t* mv, const QTab& t_in, int zigzag,
                                  int32_t* out, hipStream_t s) {
   if (nframes <= 0) return hipSuccess;
-  QTab t = t_in;
-  qtab_prepare_fused(t);
+  const QTab& t = t_in;
   FusedArgs a = make_fused_args(frames, mv, out, nframes, H, W, sr, t);
   const int64_t ntiles = nframes * (int64_t)a.h * a.tpr;
-  launch_fused_zz<int16_t, double, double, 1, true, SRC_INTER>(a, t, zigzag,
-                                                               grid_for(ntiles, 1, 8), s);
+  if (ntiles >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit tile indices
+  launch_fused_zz<int16_t, double, double, 1, true, SRC_INTER>(a, t, zigzag, ntiles, s);
   return hipGetLastError();
 }
 
