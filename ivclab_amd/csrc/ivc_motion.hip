@@ -154,6 +154,142 @@ __global__ __launch_bounds__(256) void me_generic_kernel(const T* __restrict__ r
   }
 }
 
+// ---------------------------------------------------------------- fast exact u8 search
+// Integer-valued u8 frames (IVC_ME_EXACT_U8 — the reference run on frame.astype(float64),
+// videocodec.py:38), search range SR in {4, 8, 16}.
+//   SSD(b, d) = sum(c^2) + S2(d) - 2 X(b, d),  S2(d) = sum of r^2 over the window,
+//   X(b, d)   = sum c*r  (v_dot4_u32_u8: 4 byte MACs per instruction).
+// sum(c^2) is constant per block, so K = S2 - 2X orders the candidates exactly like the SSD
+// (every term is an exact integer < 2^24): same minimum, same ties, same raster tie-break.
+// A workgroup owns BX = 256 / (2SR+1) consecutive blocks of one block row; thread
+// (b, dyi) evaluates the 2SR+1 dx candidates of one dy for block b.  The reference window
+// of the workgroup sits in LDS as dwords; the 4 byte-shifts of each ref row are built
+// with v_alignbyte and reused by the thread's 2SR+1 candidates.  S2 comes from LDS box
+// sums (horizontal then vertical 8-sums of r^2).
+template <int SR>
+__global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restrict__ ref,
+                                                         const uint8_t* __restrict__ cur,
+                                                         int64_t nframes, int H, int W,
+                                                         int64_t* __restrict__ mv) {
+  constexpr int N = 2 * SR + 1;             // candidates per axis
+  constexpr int BX = 256 / N;               // blocks per workgroup
+  constexpr int NGX = (N + 3) / 4;          // dx groups of 4
+  constexpr int NW = NGX + 2;               // ref dwords a thread reads per row
+  constexpr int RH = 8 + 2 * SR;            // ref region rows
+  constexpr int RWD = 2 * BX + NW;          // ref region width in dwords (>= 8BX+2SR bytes)
+  constexpr int NPOS = 8 * (BX - 1) + N;    // window x-positions per row
+  static_assert(SR % 4 == 0, "region start must be dword aligned");
+  __shared__ uint32_t sref[RH * RWD];
+  __shared__ uint32_t scur[BX * 16];
+  __shared__ int sh2[RH * NPOS];
+  __shared__ int ss2[N * NPOS];
+  __shared__ int sk[256];
+  __shared__ int si[256];
+  const int tid = threadIdx.x;
+  const int h = H / 8, w = W / 8;
+  const int tpr = (w + BX - 1) / BX;
+  const int64_t ntiles = nframes * h * tpr;
+  const int64_t HW = (int64_t)H * W;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t f = tile / ((int64_t)h * tpr);
+    const int rem = (int)(tile - f * h * tpr);
+    const int by = rem / tpr, bx0 = (rem - by * tpr) * BX;
+    const int y0 = 8 * by - SR, x0 = 8 * bx0 - SR;
+    const uint8_t* R = ref + f * HW;
+    const uint8_t* Cf = cur + f * HW;
+    // ---- stage the reference window (zeros outside the frame) and the current blocks ---
+    for (int i = tid; i < RH * RWD; i += 256) {
+      const int row = i / RWD, dw = i - row * RWD;
+      const int gy = y0 + row, gx = x0 + 4 * dw;
+      uint32_t v = 0;
+      if (gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W)
+        v = *reinterpret_cast<const uint32_t*>(R + (int64_t)gy * W + gx);
+      sref[i] = v;
+    }
+    for (int i = tid; i < BX * 16; i += 256) {
+      const int blk = i >> 4, row = (i >> 1) & 7, half = i & 1;
+      const int bx = bx0 + blk;
+      uint32_t v = 0;
+      if (bx < w) v = *reinterpret_cast<const uint32_t*>(Cf + (int64_t)(8 * by + row) * W + 8 * bx + 4 * half);
+      scur[i] = v;
+    }
+    __syncthreads();
+    // ---- window sums of squares: horizontal 8-sums, then vertical ------------------------
+    for (int i = tid; i < RH * NPOS; i += 256) {
+      const int row = i / NPOS, c = i - row * NPOS;
+      const uint32_t* rw = sref + row * RWD;
+      const int d0 = c >> 2, sh = c & 3;
+      const uint32_t lo = __builtin_amdgcn_alignbyte(rw[d0 + 1], rw[d0], sh);
+      const uint32_t hi = __builtin_amdgcn_alignbyte(rw[d0 + 2], rw[d0 + 1], sh);
+      sh2[i] = (int)__builtin_amdgcn_udot4(hi, hi, __builtin_amdgcn_udot4(lo, lo, 0u, false), false);
+    }
+    __syncthreads();
+    for (int i = tid; i < N * NPOS; i += 256) {
+      const int dyi = i / NPOS, c = i - dyi * NPOS;
+      int sum = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sum += sh2[(dyi + u) * NPOS + c];
+      ss2[i] = sum;
+    }
+    __syncthreads();
+    // ---- cross terms: thread (b, dyi) over all dx ----------------------------------------
+    int bestk = 0x7fffffff, besti = 0x7fffffff;
+    const int b = tid / N, dyi = tid - b * N;
+    const int bx = bx0 + b;
+    if (b < BX && bx < w) {
+      const int dy = dyi - SR;
+      const bool vy = 8 * by + dy >= 0 && 8 * by + dy + 8 <= H;
+      if (vy) {
+        uint32_t cw[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) cw[k] = scur[b * 16 + k];
+        uint32_t acc[NGX * 4];
+#pragma unroll
+        for (int k = 0; k < NGX * 4; ++k) acc[k] = 0;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const uint32_t* rw = sref + (dyi + u) * RWD + 2 * b;
+          uint32_t wv[NW];
+#pragma unroll
+          for (int j = 0; j < NW; ++j) wv[j] = rw[j];
+#pragma unroll
+          for (int g = 0; g < NGX; ++g) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              const uint32_t lo = s == 0 ? wv[g] : __builtin_amdgcn_alignbyte(wv[g + 1], wv[g], s);
+              const uint32_t hi = s == 0 ? wv[g + 1] : __builtin_amdgcn_alignbyte(wv[g + 2], wv[g + 1], s);
+              acc[4 * g + s] = __builtin_amdgcn_udot4(lo, cw[2 * u], acc[4 * g + s], false);
+              acc[4 * g + s] = __builtin_amdgcn_udot4(hi, cw[2 * u + 1], acc[4 * g + s], false);
+            }
+          }
+        }
+        const int* s2 = ss2 + dyi * NPOS + 8 * b;
+#pragma unroll
+        for (int dxi = 0; dxi < N; ++dxi) {
+          const int dx = dxi - SR;
+          const bool vx = 8 * bx + dx >= 0 && 8 * bx + dx + 8 <= W;
+          const int k = s2[dxi] - 2 * (int)acc[dxi];
+          const bool better = vx && k < bestk;
+          bestk = better ? k : bestk;
+          besti = better ? dyi * N + dxi : besti;
+        }
+      }
+    }
+    sk[tid] = bestk;
+    si[tid] = besti;
+    __syncthreads();
+    if (tid < BX && bx0 + tid < w) {
+      int bk = 0x7fffffff, bi = 0x7fffffff;
+      for (int d = 0; d < N; ++d) {   // dy order: first strict minimum = lowest raster index
+        const int i = si[tid * N + d];
+        if (i != 0x7fffffff && (bi == 0x7fffffff || sk[tid * N + d] < bk)) { bk = sk[tid * N + d]; bi = i; }
+      }
+      mv[(f * h + by) * w + bx0 + tid] = bi == 0x7fffffff ? (int64_t)SR * N + SR : (int64_t)bi;
+    }
+    __syncthreads();
+  }
+}
+
 hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, int64_t nframes,
                                   int64_t H, int64_t W, int sr, int mode, int64_t* mv,
                                   hipStream_t s) {
@@ -165,7 +301,16 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
   me_generic_kernel<T, M><<<grid, 256, 0, s>>>((const T*)ref, (const T*)cur, nframes, h, w, sr, mv)
   if (mode == IVC_ME_EXACT_U8) {
     if (dtype != IVC_U8) return hipErrorInvalidValue;
-    ME_LAUNCH(uint8_t, 1);
+    const int64_t rows = nframes * (H / 8);
+    switch (sr) {
+      case 4: me_fast_u8_kernel<4><<<me_grid(rows * ((W / 8 + 27) / 28), 1, 8), 256, 0, s>>>(
+                  (const uint8_t*)ref, (const uint8_t*)cur, nframes, h, w, mv); break;
+      case 8: me_fast_u8_kernel<8><<<me_grid(rows * ((W / 8 + 14) / 15), 1, 8), 256, 0, s>>>(
+                  (const uint8_t*)ref, (const uint8_t*)cur, nframes, h, w, mv); break;
+      case 16: me_fast_u8_kernel<16><<<me_grid(rows * ((W / 8 + 6) / 7), 1, 8), 256, 0, s>>>(
+                  (const uint8_t*)ref, (const uint8_t*)cur, nframes, h, w, mv); break;
+      default: ME_LAUNCH(uint8_t, 1); break;
+    }
     return hipGetLastError();
   }
   if (mode != IVC_ME_NUMPY) return hipErrorInvalidValue;

@@ -1,0 +1,53 @@
+"""Frame sharding and the histogram exchange for multi-GPU runs (one process per GPU).
+
+The block-codec hot path has no data-path collective: intra frames are independent and,
+in the open-loop sequence benchmark, so are frame pairs (f-1, f).  The one exchange is the
+input of the global Huffman table: every rank histograms its own symbols
+on its GPU and the ranks all-gather the int64 histograms, then sum them in rank order
+(integer, hence identical on every rank and independent of arrival order).
+torch.distributed is the transport (backend "nccl" = RCCL over xGMI on MI355X; "gloo" in
+the CPU tests).
+"""
+from __future__ import annotations
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple:
+    """Contiguous [start, stop) share of n items for `rank` (sizes differ by at most 1)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("rank must be in [0, world)")
+    q, r = divmod(n, world)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def shard_pairs(nframes: int, rank: int, world: int) -> tuple:
+    """Frames a rank needs for its share of the nframes-1 consecutive pairs (f-1, f) of a
+    sequence: returns (first_frame, stop_frame) including the one-frame halo, so the rank
+    runs inter coding on frames[first:stop] and produces pairs first+1 .. stop-1."""
+    s, e = shard_range(max(nframes - 1, 0), rank, world)
+    if s == e:
+        return s, s
+    return s, e + 1
+
+
+def global_histogram(local_hist, group=None):
+    """Sum of every rank's histogram (a 1-D int64 tensor on this rank's device) via one
+    all-gather; every rank receives the same result."""
+    import torch
+    import torch.distributed as dist
+    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return local_hist.clone()
+    world = dist.get_world_size(group)
+    gathered = torch.empty((world,) + tuple(local_hist.shape), dtype=local_hist.dtype,
+                           device=local_hist.device)
+    try:
+        dist.all_gather_into_tensor(gathered, local_hist.contiguous(), group=group)
+    except (RuntimeError, NotImplementedError):
+        # backends without the fused form (older gloo): same exchange as a list all-gather
+        parts = [torch.empty_like(local_hist) for _ in range(world)]
+        dist.all_gather(parts, local_hist.contiguous(), group=group)
+        gathered = torch.stack(parts)
+    total = gathered[0].clone()
+    for k in range(1, world):           # rank order: deterministic integer sum
+        total += gathered[k]
+    return total

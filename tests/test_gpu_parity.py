@@ -357,3 +357,39 @@ def test_device_api_intra_and_inter():
     for f in range(F):
         assert_bits(qi[f], O.intra_encode(frames[f][..., None], 1.0, zigzag=True), f"intra {f}")
     assert np.array_equal(hist, O.histogram(qi, -4096, 8192))
+
+
+@pytest.mark.parametrize("sr", [4, 8, 16, 5])
+@pytest.mark.parametrize("shape", [(16, 16), (72, 264), (136, 120), (8, 224)])
+def test_me_exact_u8_fast_paths(sr, shape):
+    """Exact-u8 mode (fast dot4 kernel for sr in {4, 8, 16}, generic otherwise) against the
+    C oracle on the float64 frames: random, shifted, flat (all-tie) and edge-heavy sizes."""
+    import ivclab_amd._native as N
+    rng = np.random.default_rng(sr * 1000 + shape[1])
+    H, W = shape
+    base = rng.integers(0, 256, (H + 40, W + 40), dtype=np.uint8)
+    cases = [(base[:H, :W], base[3:H + 3, 5:W + 5]),
+             (np.full((H, W), 77, np.uint8), np.full((H, W), 77, np.uint8)),
+             (base[:H, :W], np.zeros((H, W), np.uint8))]
+    for ref, cur in cases:
+        ref, cur = np.ascontiguousarray(ref), np.ascontiguousarray(cur)
+        mv = np.empty((H // 8, W // 8, 1), np.int64)
+        N.check(N.lib().ivc_motion_estimate(N.ptr(ref), N.ptr(cur), 1, 1, H, W, sr, N.ME_EXACT_U8, N.ptr(mv)))
+        want = c_motion_vectors(ref.astype(np.float64), cur.astype(np.float64), sr)
+        assert_bits(mv, want.astype(np.int64), f"exact u8 sr={sr} {shape}")
+
+
+def test_me_exact_u8_full_hd_vs_c_oracle():
+    """A full 1080p pair at sr=16 (the bench configuration), checked on sampled block rows
+    (top, middle, bottom) against the C oracle."""
+    import ivclab_amd._native as N
+    rng = np.random.default_rng(1080)
+    lo = rng.integers(0, 256, (290, 500)).astype(np.float64)
+    big = np.kron(lo, np.ones((4, 4)))[:1120, :1960] + rng.integers(-8, 9, (1120, 1960))
+    big = np.clip(big, 0, 255).astype(np.uint8)
+    ref, cur = np.ascontiguousarray(big[:1080, :1920]), np.ascontiguousarray(big[3:1083, 7:1927])
+    mv = np.empty((135, 240, 1), np.int64)
+    N.check(N.lib().ivc_motion_estimate(N.ptr(ref), N.ptr(cur), 1, 1, 1080, 1920, 16, N.ME_EXACT_U8, N.ptr(mv)))
+    for rows in ((0, 3), (66, 69), (132, 135)):
+        want = c_motion_vectors(ref, cur, 16, exact_u8=True, rows=rows)
+        assert_bits(mv[rows[0]:rows[1]], want.astype(np.int64), f"1080p rows {rows}")
