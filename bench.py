@@ -181,6 +181,7 @@ def main():
     ap.add_argument("--sr", type=int, default=16)
     ap.add_argument("--zigzag", action="store_true")
     ap.add_argument("--no-inter", action="store_true")
+    ap.add_argument("--no-intra", action="store_true", help="profiling aid: skip the cfg3 leg")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 
@@ -192,6 +193,8 @@ def main():
 
     # ---- cfg3: 4K intra DCT + quant -------------------------------------------------------
     F, H, W = args.frames, args.height, args.width
+    if args.no_intra:
+        F = 1
     frames = intra_frames(F, H, W, seed=3 + 1000 * rank, dev=dev).view(F, H, W, 1)
     out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
 

@@ -18,6 +18,27 @@
 
 namespace ivc {
 
+// per-device scratch for the S2 pre-pass (grown on demand, never shrunk; one stream at a
+// time per device is assumed for this buffer, like the host-staging scratch in the C-ABI)
+static int32_t* g_s2[64] = {};
+static size_t g_s2_cap[64] = {};
+static int32_t* me_s2_scratch(int64_t elems, hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  const size_t bytes = (size_t)elems * 4;
+  if (g_s2_cap[dev] < bytes) {
+    if (g_s2[dev]) {
+      (void)hipStreamSynchronize(s);
+      (void)hipFree(g_s2[dev]);
+    }
+    g_s2[dev] = nullptr;
+    g_s2_cap[dev] = 0;
+    if (hipMalloc(&g_s2[dev], bytes) != hipSuccess) return nullptr;
+    g_s2_cap[dev] = bytes;
+  }
+  return g_s2[dev];
+}
+
 static int g_cus = 0;
 static unsigned me_grid(int64_t items, int per_block, int max_per_cu) {
   if (g_cus == 0) {
@@ -161,132 +182,282 @@ __global__ __launch_bounds__(256) void me_generic_kernel(const T* __restrict__ r
 //   X(b, d)   = sum c*r  (v_dot4_u32_u8: 4 byte MACs per instruction).
 // sum(c^2) is constant per block, so K = S2 - 2X orders the candidates exactly like the SSD
 // (every term is an exact integer < 2^24): same minimum, same ties, same raster tie-break.
-// A workgroup owns BX = 256 / (2SR+1) consecutive blocks of one block row; thread
-// (b, dyi) evaluates the 2SR+1 dx candidates of one dy for block b.  The reference window
-// of the workgroup sits in LDS as dwords; the 4 byte-shifts of each ref row are built
-// with v_alignbyte and reused by the thread's 2SR+1 candidates.  S2 comes from LDS box
-// sums (horizontal then vertical 8-sums of r^2).
-template <int SR>
-__global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restrict__ ref,
-                                                         const uint8_t* __restrict__ cur,
-                                                         int64_t nframes, int H, int W,
-                                                         int64_t* __restrict__ mv) {
-  constexpr int N = 2 * SR + 1;             // candidates per axis
-  constexpr int BX = 256 / N;               // blocks per workgroup
-  constexpr int NGX = (N + 3) / 4;          // dx groups of 4
-  constexpr int NW = NGX + 2;               // ref dwords a thread reads per row
-  constexpr int RH = 8 + 2 * SR;            // ref region rows
-  constexpr int RWD = 2 * BX + NW;          // ref region width in dwords (>= 8BX+2SR bytes)
-  constexpr int NPOS = 8 * (BX - 1) + N;    // window x-positions per row
-  static_assert(SR % 4 == 0, "region start must be dword aligned");
-  __shared__ uint32_t sref[RH * RWD];
-  __shared__ uint32_t scur[BX * 16];
-  __shared__ int sh2[RH * NPOS];
-  __shared__ int ss2[N * NPOS];
-  __shared__ int sk[256];
-  __shared__ int si[256];
-  const int tid = threadIdx.x;
-  const int h = H / 8, w = W / 8;
-  const int tpr = (w + BX - 1) / BX;
-  const int64_t ntiles = nframes * h * tpr;
+//
+// S2 comes from a box-filter pre-pass over each reference frame (me_s2_kernel).  The search
+// is wave-independent: a wave owns BPW adjacent blocks; lane (block, g, dr) evaluates the
+// DYT x 4 candidates dy in [dr*DYT, dr*DYT + DYT) x dx in [4g, 4g + 4) of its block.  The
+// blocks' reference windows are staged in a wave-private LDS region (no barrier), the next
+// group's windows are prefetched into registers while the current one is searched, the
+// 4 byte-shifts of a ref row come from v_alignbyte and serve all of the lane's dy, and the
+// lexicographic (K, raster index) minimum is reduced across the block's lanes with
+// shuffles.
+
+// S2[f][y][x] = sum of squares of the 8x8 window with top-left (y, x), for y <= H-8, x <= W-8.
+// Thread = 4 consecutive x of one frame and a run of S2Y output rows: the horizontal
+// 8-sums of r^2 come from dot4 on byte-shifted dwords, the vertical 8-sum slides down the
+// run with the last 8 horizontal sums kept in registers.
+constexpr int S2Y = 64;
+
+__device__ __forceinline__ void s2_hrow(__amdgpu_buffer_rsrc_t rs, int off, uint32_t* hs) {
+  const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+  const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 4, 0, 0);
+  const uint32_t w2 = __builtin_amdgcn_raw_buffer_load_b32(rs, off + 8, 0, 0);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const uint32_t lo = s == 0 ? w0 : __builtin_amdgcn_alignbyte(w1, w0, s);
+    const uint32_t hi = s == 0 ? w1 : __builtin_amdgcn_alignbyte(w2, w1, s);
+    hs[s] = __builtin_amdgcn_udot4(hi, hi, __builtin_amdgcn_udot4(lo, lo, 0u, false), false);
+  }
+}
+
+__global__ __launch_bounds__(256) void me_s2_kernel(const uint8_t* __restrict__ ref,
+                                                    int64_t nframes, int H, int W,
+                                                    int32_t* __restrict__ s2) {
+  const int nx = (W - 8) / 4 + 1;                  // x groups covering x = 0 .. W-8
+  const int ny = (H - 8) / S2Y + 1;                // row runs covering y = 0 .. H-8
+  const int64_t total = nframes * (int64_t)nx * ny;
   const int64_t HW = (int64_t)H * W;
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t f = tile / ((int64_t)h * tpr);
-    const int rem = (int)(tile - f * h * tpr);
-    const int by = rem / tpr, bx0 = (rem - by * tpr) * BX;
-    const int y0 = 8 * by - SR, x0 = 8 * bx0 - SR;
-    const uint8_t* R = ref + f * HW;
-    const uint8_t* Cf = cur + f * HW;
-    // ---- stage the reference window (zeros outside the frame) and the current blocks ---
-    for (int i = tid; i < RH * RWD; i += 256) {
-      const int row = i / RWD, dw = i - row * RWD;
-      const int gy = y0 + row, gx = x0 + 4 * dw;
-      uint32_t v = 0;
-      if (gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W)
-        v = *reinterpret_cast<const uint32_t*>(R + (int64_t)gy * W + gx);
-      sref[i] = v;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * 256) {
+    const int xg = (int)(i % nx);
+    const int64_t t = i / nx;
+    const int yr = (int)(t % ny);
+    const int64_t f = t / ny;
+    const int x = 4 * xg, y0 = yr * S2Y;
+    const int y1 = min(y0 + S2Y, H - 7);          // exclusive
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(ref + f * HW), 0, (int)HW, 0x00020000);
+    int32_t* out = s2 + f * HW + x;
+    const int nvalid = min(4, W - 7 - x);         // outputs of this group inside the row
+    uint32_t h[8][4];
+    uint32_t acc[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      s2_hrow(rs, (y0 + k) * W + x, h[k]);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[s] += h[k][s];
     }
-    for (int i = tid; i < BX * 16; i += 256) {
-      const int blk = i >> 4, row = (i >> 1) & 7, half = i & 1;
-      const int bx = bx0 + blk;
-      uint32_t v = 0;
-      if (bx < w) v = *reinterpret_cast<const uint32_t*>(Cf + (int64_t)(8 * by + row) * W + 8 * bx + 4 * half);
-      scur[i] = v;
-    }
-    __syncthreads();
-    // ---- window sums of squares: horizontal 8-sums, then vertical ------------------------
-    for (int i = tid; i < RH * NPOS; i += 256) {
-      const int row = i / NPOS, c = i - row * NPOS;
-      const uint32_t* rw = sref + row * RWD;
-      const int d0 = c >> 2, sh = c & 3;
-      const uint32_t lo = __builtin_amdgcn_alignbyte(rw[d0 + 1], rw[d0], sh);
-      const uint32_t hi = __builtin_amdgcn_alignbyte(rw[d0 + 2], rw[d0 + 1], sh);
-      sh2[i] = (int)__builtin_amdgcn_udot4(hi, hi, __builtin_amdgcn_udot4(lo, lo, 0u, false), false);
-    }
-    __syncthreads();
-    for (int i = tid; i < N * NPOS; i += 256) {
-      const int dyi = i / NPOS, c = i - dyi * NPOS;
-      int sum = 0;
+    for (int y = y0; y < y1; y += 8) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) sum += sh2[(dyi + u) * NPOS + c];
-      ss2[i] = sum;
-    }
-    __syncthreads();
-    // ---- cross terms: thread (b, dyi) over all dx ----------------------------------------
-    int bestk = 0x7fffffff, besti = 0x7fffffff;
-    const int b = tid / N, dyi = tid - b * N;
-    const int bx = bx0 + b;
-    if (b < BX && bx < w) {
-      const int dy = dyi - SR;
-      const bool vy = 8 * by + dy >= 0 && 8 * by + dy + 8 <= H;
-      if (vy) {
-        uint32_t cw[16];
+      for (int k = 0; k < 8; ++k) {
+        const int yy = y + k;
+        if (yy < y1) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) cw[k] = scur[b * 16 + k];
-        uint32_t acc[NGX * 4];
-#pragma unroll
-        for (int k = 0; k < NGX * 4; ++k) acc[k] = 0;
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const uint32_t* rw = sref + (dyi + u) * RWD + 2 * b;
-          uint32_t wv[NW];
-#pragma unroll
-          for (int j = 0; j < NW; ++j) wv[j] = rw[j];
-#pragma unroll
-          for (int g = 0; g < NGX; ++g) {
+          for (int s = 0; s < 4; ++s)
+            if (s < nvalid) out[(int64_t)yy * W + s] = (int32_t)acc[s];
+          if (yy + 1 < y1) {                       // slide: drop row yy, add row yy + 8
+            uint32_t hn[4];
+            s2_hrow(rs, (yy + 8) * W + x, hn);
 #pragma unroll
             for (int s = 0; s < 4; ++s) {
-              const uint32_t lo = s == 0 ? wv[g] : __builtin_amdgcn_alignbyte(wv[g + 1], wv[g], s);
-              const uint32_t hi = s == 0 ? wv[g + 1] : __builtin_amdgcn_alignbyte(wv[g + 2], wv[g + 1], s);
-              acc[4 * g + s] = __builtin_amdgcn_udot4(lo, cw[2 * u], acc[4 * g + s], false);
-              acc[4 * g + s] = __builtin_amdgcn_udot4(hi, cw[2 * u + 1], acc[4 * g + s], false);
+              acc[s] += hn[s] - h[k][s];
+              h[k][s] = hn[s];
             }
           }
         }
-        const int* s2 = ss2 + dyi * NPOS + 8 * b;
+      }
+    }
+  }
+}
+
+template <int SR> struct MeCfg;
+// PITCH: LDS row pitch of a staged window (dwords), chosen so a row read of a 32-lane half
+// hits distinct banks (searched offline; SR = 4 is 2-way at best with 4 blocks per wave)
+template <> struct MeCfg<16> { static constexpr int BPW = 1, NDR = 7, DYT = 5, PITCH = 21; };  // 63 of 64 lanes
+template <> struct MeCfg<8> { static constexpr int BPW = 2, NDR = 6, DYT = 3, PITCH = 9; };   // 30 of 32 lanes
+template <> struct MeCfg<4> { static constexpr int BPW = 4, NDR = 5, DYT = 2, PITCH = 5; };   // 15 of 16 lanes
+
+typedef unsigned int me_u32x4 __attribute__((ext_vector_type(4)));
+
+template <int DYT> __device__ __forceinline__ void row_fence(uint32_t (&acc)[DYT][4]);
+template <> __device__ __forceinline__ void row_fence<5>(uint32_t (&a)[5][4]) {
+  asm volatile("" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[1][0]),
+               "+v"(a[1][1]), "+v"(a[1][2]), "+v"(a[1][3]), "+v"(a[2][0]), "+v"(a[2][1]),
+               "+v"(a[2][2]), "+v"(a[2][3]), "+v"(a[3][0]), "+v"(a[3][1]), "+v"(a[3][2]),
+               "+v"(a[3][3]), "+v"(a[4][0]), "+v"(a[4][1]), "+v"(a[4][2]), "+v"(a[4][3])
+               :: "memory");
+}
+template <> __device__ __forceinline__ void row_fence<3>(uint32_t (&a)[3][4]) {
+  asm volatile("" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[1][0]),
+               "+v"(a[1][1]), "+v"(a[1][2]), "+v"(a[1][3]), "+v"(a[2][0]), "+v"(a[2][1]),
+               "+v"(a[2][2]), "+v"(a[2][3]) :: "memory");
+}
+template <> __device__ __forceinline__ void row_fence<2>(uint32_t (&a)[2][4]) {
+  asm volatile("" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[1][0]),
+               "+v"(a[1][1]), "+v"(a[1][2]), "+v"(a[1][3]) :: "memory");
+}
+
+template <int SR>
+__global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restrict__ ref,
+                                                         const uint8_t* __restrict__ cur,
+                                                         const int32_t* __restrict__ s2,
+                                                         int64_t nframes, int H, int W,
+                                                         int64_t* __restrict__ mv) {
+  typedef MeCfg<SR> Cfg;
+  constexpr int N = 2 * SR + 1;             // candidates per axis
+  constexpr int NGX = (N + 3) / 4;          // dx groups of 4
+  constexpr int BPW = Cfg::BPW, NDR = Cfg::NDR, DYT = Cfg::DYT;
+  constexpr int SEG = 64 / BPW;             // lanes per block (aligned segment)
+  constexpr int LPB = NGX * NDR;            // active lanes per block
+  constexpr int NW = NGX + 2;               // window width in dwords (>= 8 + 2SR bytes + 3)
+  constexpr int WR = 8 + 2 * SR;            // window rows
+  constexpr int WIN = WR * NW;              // window dwords fetched per block
+  constexpr int P = Cfg::PITCH;             // LDS row pitch (>= NW)
+  constexpr int WINL = WR * P;              // LDS dwords per block window
+  constexpr int PW = (BPW * WIN + 63) / 64; // window dwords staged per lane
+  constexpr int CUR = BPW * 16;             // cur dwords per group (<= 64)
+  constexpr int STAGE = BPW * WINL + CUR;
+  static_assert(P >= NW, "pitch");
+  static_assert(LPB <= SEG && CUR <= 64, "lanes");
+  static_assert(NDR * DYT >= N, "dy coverage");
+  static_assert(SR % 4 == 0, "window start must be dword aligned");
+  __shared__ uint32_t lds[4 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+  uint32_t* st = lds + wave * STAGE;
+  const int h = H / 8, w = W / 8;
+  const int gpr = (w + BPW - 1) / BPW;                   // block groups per block row
+  const uint32_t gpf = (uint32_t)(h * gpr);
+  const uint32_t ngroups = (uint32_t)nframes * gpf;
+  const uint32_t nwaves = gridDim.x * 4u;
+  const int64_t HW = (int64_t)H * W;
+  // lane role: block lb on lanes [lb*SEG, lb*SEG + LPB), lane lr -> (dx group g, dy range dr)
+  const int lb = lane / SEG, lr = lane - lb * SEG;
+  const int g = lr % NGX, dr = lr / NGX;
+  const bool active = lr < LPB;
+
+  // window dwords (block-major) then the BPW current blocks (8 rows x 2 dwords each)
+  auto fetch = [&](uint32_t grp, bool exists, uint32_t* wreg, uint32_t& creg) {
+    const uint32_t gg = exists ? grp : 0u;
+    const uint32_t f = gg / gpf;
+    const uint32_t rem = gg - f * gpf;
+    const int by = (int)(rem / (uint32_t)gpr);
+    const int bx0 = (int)(rem - (uint32_t)by * gpr) * BPW;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(ref + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(cur + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
 #pragma unroll
-        for (int dxi = 0; dxi < N; ++dxi) {
-          const int dx = dxi - SR;
-          const bool vx = 8 * bx + dx >= 0 && 8 * bx + dx + 8 <= W;
-          const int k = s2[dxi] - 2 * (int)acc[dxi];
-          const bool better = vx && k < bestk;
+    for (int j = 0; j < PW; ++j) {
+      const int e = lane + 64 * j;
+      const int blk = e / WIN, o = e - blk * WIN;
+      const int row = o / NW, dw = o - row * NW;
+      const int gy = 8 * by - SR + row, gx = 8 * (bx0 + blk) - SR + 4 * dw;
+      const bool ok = e < BPW * WIN && bx0 + blk < w && gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W;
+      wreg[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, ok ? gy * W + gx : 0x40000000, 0, 0);
+    }
+    const int blk = lane >> 4, c = lane & 15;
+    const bool okc = lane < CUR && bx0 + blk < w;
+    creg = __builtin_amdgcn_raw_buffer_load_b32(
+        rc, okc ? (8 * by + (c >> 1)) * W + 8 * (bx0 + blk) + 4 * (c & 1) : 0x40000000, 0, 0);
+  };
+
+  uint32_t grp = blockIdx.x * 4u + wave;
+  uint32_t wraw[PW], craw;
+  fetch(grp, grp < ngroups, wraw, craw);
+  for (; grp < ngroups; grp += nwaves) {
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const int e = lane + 64 * j;
+      const int blk = e / WIN, o = e - blk * WIN, row = o / NW;
+      if (e < BPW * WIN) st[blk * WINL + row * P + (o - row * NW)] = wraw[j];
+    }
+    if (lane < CUR) st[BPW * WINL + lane] = craw;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t ng = grp + nwaves;
+    fetch(ng, ng < ngroups, wraw, craw);                   // prefetch the next group
+
+    const uint32_t f = grp / gpf;
+    const uint32_t rem = grp - f * gpf;
+    const int by = (int)(rem / (uint32_t)gpr);
+    const int bx = (int)(rem - (uint32_t)by * gpr) * BPW + lb;
+    int bestk = 0x7fffffff, besti = 0x7fffffff;
+    if (active && bx < w) {
+      const uint32_t* win = st + lb * WINL;
+      const uint32_t* cb = st + BPW * WINL + lb * 16;
+      uint32_t cw[16];
+#pragma unroll
+      for (int k = 0; k < 16; ++k) cw[k] = cb[k];
+      uint32_t acc[DYT][4];
+#pragma unroll
+      for (int d = 0; d < DYT; ++d)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[d][s] = 0;
+      const int dy0 = dr * DYT;
+      // row words are read one row ahead of their use (the fence below would otherwise
+      // expose the LDS latency once per row)
+      auto row_words = [&](int row, uint32_t& a0, uint32_t& a1, uint32_t& a2) {
+        const bool in = row < WR;
+        const uint32_t* p = win + (in ? row : 0) * P + g;
+        a0 = p[0]; a1 = p[1]; a2 = p[2];
+        if (!in) { a0 = 0u; a1 = 0u; a2 = 0u; }
+      };
+      uint32_t w0, w1, w2;
+      row_words(dy0, w0, w1, w2);
+#pragma unroll
+      for (int rr = 0; rr < DYT + 7; ++rr) {
+        uint32_t n0 = 0u, n1 = 0u, n2 = 0u;
+        if (rr + 1 < DYT + 7) row_words(dy0 + rr + 1, n0, n1, n2);
+        uint32_t lo[4], hi[4];
+        lo[0] = w0; hi[0] = w1;
+#pragma unroll
+        for (int s = 1; s < 4; ++s) {
+          lo[s] = __builtin_amdgcn_alignbyte(w1, w0, s);
+          hi[s] = __builtin_amdgcn_alignbyte(w2, w1, s);
+        }
+#pragma unroll
+        for (int d = 0; d < DYT; ++d) {
+          const int u = rr - d;                          // block row matched by this ref row
+          if (u >= 0 && u < 8) {
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+              acc[d][s] = __builtin_amdgcn_udot4(lo[s], cw[2 * u], acc[d][s], false);
+              acc[d][s] = __builtin_amdgcn_udot4(hi[s], cw[2 * u + 1], acc[d][s], false);
+            }
+          }
+        }
+        // keep the schedule row by row: the compiler otherwise hoists every row's LDS reads
+        // and byte shifts ahead of the dot products (~100 more live registers, 3 waves per
+        // SIMD instead of 6); the empty asm pins the row's accumulators and orders memory
+        row_fence<DYT>(acc);
+        w0 = n0; w1 = n1; w2 = n2;
+      }
+      // the lane's candidates in raster order (dy outer, dx inner): first strict minimum
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<int32_t*>(s2 + (int64_t)f * HW), 0, (int)(HW * 4), 0x00020000);
+#pragma unroll
+      for (int d = 0; d < DYT; ++d) {
+        const int dyi = dy0 + d;
+        const int ry = 8 * by + dyi - SR, rx0 = 8 * bx + 4 * g - SR;
+        const bool vy = dyi < N && ry >= 0 && ry + 8 <= H;
+        // rx0 is a multiple of 4, so rx0 < 0 means all four candidates are off-frame
+        const me_u32x4 sq = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, vy && rx0 >= 0 ? (ry * W + rx0) * 4 : 0x40000000, 0, 0);
+        const uint32_t sv[4] = {sq.x, sq.y, sq.z, sq.w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int dxi = 4 * g + s;
+          const int rx = rx0 + s;
+          const bool valid = vy && dxi < N && rx >= 0 && rx + 8 <= W;
+          const int k = (int)sv[s] - 2 * (int)acc[d][s];
+          const bool better = valid && k < bestk;
           bestk = better ? k : bestk;
           besti = better ? dyi * N + dxi : besti;
         }
       }
     }
-    sk[tid] = bestk;
-    si[tid] = besti;
-    __syncthreads();
-    if (tid < BX && bx0 + tid < w) {
-      int bk = 0x7fffffff, bi = 0x7fffffff;
-      for (int d = 0; d < N; ++d) {   // dy order: first strict minimum = lowest raster index
-        const int i = si[tid * N + d];
-        if (i != 0x7fffffff && (bi == 0x7fffffff || sk[tid * N + d] < bk)) { bk = sk[tid * N + d]; bi = i; }
-      }
-      mv[(f * h + by) * w + bx0 + tid] = bi == 0x7fffffff ? (int64_t)SR * N + SR : (int64_t)bi;
+    // lexicographic (K, index) minimum over the block's aligned lane segment; lanes with no
+    // candidate carry (INT_MAX, INT_MAX)
+#pragma unroll
+    for (int off = 1; off < SEG; off <<= 1) {
+      const int ok_ = __shfl_xor(bestk, off), oi = __shfl_xor(besti, off);
+      const bool take = ok_ < bestk || (ok_ == bestk && oi < besti);
+      bestk = take ? ok_ : bestk;
+      besti = take ? oi : besti;
     }
-    __syncthreads();
+    if (lr == 0 && bx < w)
+      mv[((int64_t)f * h + by) * w + bx] = besti == 0x7fffffff ? (int64_t)SR * N + SR : (int64_t)besti;
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -301,14 +472,24 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
   me_generic_kernel<T, M><<<grid, 256, 0, s>>>((const T*)ref, (const T*)cur, nframes, h, w, sr, mv)
   if (mode == IVC_ME_EXACT_U8) {
     if (dtype != IVC_U8) return hipErrorInvalidValue;
-    const int64_t rows = nframes * (H / 8);
+    if (sr == 4 || sr == 8 || sr == 16) {
+      // S2 scratch: one int32 per pixel of the reference frames (library-owned, grown once)
+      int32_t* s2 = me_s2_scratch(nframes * H * W, s);
+      if (!s2) return hipErrorOutOfMemory;
+      me_s2_kernel<<<me_grid(nframes * ((W - 8) / 4 + 1) * ((H - 8) / S2Y + 1), 256, 8), 256, 0, s>>>(
+          (const uint8_t*)ref, nframes, h, w, s2);
+      const int64_t groups_bpw1 = nframes * (H / 8) * (W / 8);
+      switch (sr) {
+        case 4: me_fast_u8_kernel<4><<<me_grid((groups_bpw1 / 4 + 3) / 4, 1, 8), 256, 0, s>>>(
+                    (const uint8_t*)ref, (const uint8_t*)cur, s2, nframes, h, w, mv); break;
+        case 8: me_fast_u8_kernel<8><<<me_grid((groups_bpw1 / 2 + 3) / 4, 1, 8), 256, 0, s>>>(
+                    (const uint8_t*)ref, (const uint8_t*)cur, s2, nframes, h, w, mv); break;
+        default: me_fast_u8_kernel<16><<<me_grid((groups_bpw1 + 3) / 4, 1, 8), 256, 0, s>>>(
+                    (const uint8_t*)ref, (const uint8_t*)cur, s2, nframes, h, w, mv); break;
+      }
+      return hipGetLastError();
+    }
     switch (sr) {
-      case 4: me_fast_u8_kernel<4><<<me_grid(rows * ((W / 8 + 27) / 28), 1, 8), 256, 0, s>>>(
-                  (const uint8_t*)ref, (const uint8_t*)cur, nframes, h, w, mv); break;
-      case 8: me_fast_u8_kernel<8><<<me_grid(rows * ((W / 8 + 14) / 15), 1, 8), 256, 0, s>>>(
-                  (const uint8_t*)ref, (const uint8_t*)cur, nframes, h, w, mv); break;
-      case 16: me_fast_u8_kernel<16><<<me_grid(rows * ((W / 8 + 6) / 7), 1, 8), 256, 0, s>>>(
-                  (const uint8_t*)ref, (const uint8_t*)cur, nframes, h, w, mv); break;
       default: ME_LAUNCH(uint8_t, 1); break;
     }
     return hipGetLastError();
