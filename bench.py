@@ -188,6 +188,7 @@ def main():
     dist, rank, world, local = dist_setup(args.gpus)
     dev = torch.device("cuda", torch.cuda.current_device())
     import ivclab_amd.device as D
+    from ivclab_amd.distributed import global_histogram
     from ivclab_amd import PatchQuant
     table = PatchQuant(1.0).get_quantization_table()
 
@@ -217,12 +218,7 @@ def main():
     torch.cuda.synchronize()
     t_ex = time.perf_counter()
     D.histogram(out.view(-1), HIST_LO, hist)
-    if dist is not None:
-        gathered = torch.empty((world, HIST_BINS), dtype=torch.int64, device=dev)
-        dist.all_gather_into_tensor(gathered, hist)
-        ghist = gathered.sum(0)
-    else:
-        ghist = hist
+    ghist = global_histogram(hist)
     torch.cuda.synchronize()
     exchange_ms = (time.perf_counter() - t_ex) * 1e3
     total_syms = int(ghist.sum().item())

@@ -857,8 +857,8 @@ __global__ __launch_bounds__(256) void histogram_kernel(const int32_t* __restric
   const int64_t zb64 = (int64_t)0 - lo;
   const int zb = zb64 < 0 ? 0 : (zb64 >= nbins ? nbins - 1 : (int)zb64);
   unsigned zeros = 0;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < n; i += (int64_t)gridDim.x * 256) {
-    const int64_t b64 = (int64_t)sym[i] - lo;
+  auto count = [&](int32_t v) {
+    const int64_t b64 = (int64_t)v - lo;
     const int b = b64 < 0 ? 0 : (b64 >= nbins ? nbins - 1 : (int)b64);
     if (b == zb) {
       ++zeros;
@@ -867,7 +867,29 @@ __global__ __launch_bounds__(256) void histogram_kernel(const int32_t* __restric
     } else {
       atomicAdd(&hist[b], 1ull);
     }
+  };
+  // 16 B per lane, two loads in flight per iteration (the symbol stream is read once)
+  // a 4-byte-aligned stream that does not start on 16 B: the first `head` symbols apart
+  int64_t head = (int64_t)((16u - ((uintptr_t)sym & 15u)) & 15u) >> 2;
+  if (head > n) head = n;
+  if (blockIdx.x == 0 && tid < head) count(sym[tid]);
+  sym += head;
+  n -= head;
+  typedef int hi4 __attribute__((ext_vector_type(4)));
+  const hi4* s4 = reinterpret_cast<const hi4*>(sym);
+  const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + tid;
+  for (; i + stride < n4; i += 2 * stride) {
+    const hi4 a = __builtin_nontemporal_load(s4 + i);
+    const hi4 b = __builtin_nontemporal_load(s4 + i + stride);
+    count(a.x); count(a.y); count(a.z); count(a.w);
+    count(b.x); count(b.y); count(b.z); count(b.w);
   }
+  if (i < n4) {
+    const hi4 a = __builtin_nontemporal_load(s4 + i);
+    count(a.x); count(a.y); count(a.z); count(a.w);
+  }
+  if (blockIdx.x == 0 && tid < (int)(n & 3)) count(sym[(n4 << 2) + tid]);
   if (use_lds) {
     atomicAdd(&bins[zb], zeros);
     __syncthreads();

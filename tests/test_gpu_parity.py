@@ -330,6 +330,22 @@ def test_histogram_vs_oracle():
         assert np.array_equal(h, O.histogram(sym, lo, nb))
 
 
+def test_histogram_device_offsets_and_ragged():
+    """Device histogram on views that start off 16 B and lengths that are not multiples of 4
+    (the kernel reads 16 B per lane after an unaligned head)."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(2)
+    base = rng.integers(-300, 300, (1 << 16) + 9).astype(np.int32)
+    base[::5] = 0
+    t = torch.from_numpy(base).cuda()
+    for off in (0, 1, 2, 3):
+        for n in (0, 1, 3, 4, 5, 7, 1023, 4096 + 3, base.size - off):
+            h = torch.zeros(512, dtype=torch.int64, device="cuda")
+            D.histogram(t[off:off + n], -256, h)
+            assert np.array_equal(h.cpu().numpy(), O.histogram(base[off:off + n], -256, 512)), (off, n)
+
+
 # ------------------------------------------------------------------------ device API ---
 def test_device_api_intra_and_inter():
     torch = pytest.importorskip("torch")
