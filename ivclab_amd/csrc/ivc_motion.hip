@@ -337,14 +337,30 @@ __global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restri
         const_cast<uint8_t*>(ref + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(cur + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
+    // wave-uniform: every window of the group lies inside the frame (no per-dword checks)
+    const bool inner = 8 * by >= SR && 8 * by + 8 + SR <= H && 8 * bx0 >= SR &&
+                       8 * (bx0 + BPW) + SR <= W;
+    const int oy = 8 * by - SR, ox = 8 * bx0 - SR;
+    if (inner) {
 #pragma unroll
-    for (int j = 0; j < PW; ++j) {
-      const int e = lane + 64 * j;
-      const int blk = e / WIN, o = e - blk * WIN;
-      const int row = o / NW, dw = o - row * NW;
-      const int gy = 8 * by - SR + row, gx = 8 * (bx0 + blk) - SR + 4 * dw;
-      const bool ok = e < BPW * WIN && bx0 + blk < w && gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W;
-      wreg[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, ok ? gy * W + gx : 0x40000000, 0, 0);
+      for (int j = 0; j < PW; ++j) {
+        const int e = lane + 64 * j;
+        const int blk = e / WIN, o = e - blk * WIN;
+        const int row = o / NW, dw = o - row * NW;
+        const bool ok = (64 * j + 63 < BPW * WIN) || e < BPW * WIN;
+        wreg[j] = __builtin_amdgcn_raw_buffer_load_b32(
+            rr, ok ? (oy + row) * W + ox + 8 * blk + 4 * dw : 0x40000000, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < PW; ++j) {
+        const int e = lane + 64 * j;
+        const int blk = e / WIN, o = e - blk * WIN;
+        const int row = o / NW, dw = o - row * NW;
+        const int gy = oy + row, gx = ox + 8 * blk + 4 * dw;
+        const bool ok = e < BPW * WIN && bx0 + blk < w && gy >= 0 && gy < H && gx >= 0 && gx + 4 <= W;
+        wreg[j] = __builtin_amdgcn_raw_buffer_load_b32(rr, ok ? gy * W + gx : 0x40000000, 0, 0);
+      }
     }
     const int blk = lane >> 4, c = lane & 15;
     const bool okc = lane < CUR && bx0 + blk < w;
@@ -422,28 +438,35 @@ __global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restri
         row_fence<DYT>(acc);
         w0 = n0; w1 = n1; w2 = n2;
       }
-      // the lane's candidates in raster order (dy outer, dx inner): first strict minimum
+      // the lane's candidates in raster order (dy outer, dx inner): first strict minimum.
+      // K = S2 - 2X lies in [-64*255^2, 64*255^2] (SSD = K + sum c^2 >= 0), so
+      // 32 (K + 2^22) + (raster rank within the lane, < 32) is a positive int32 key whose
+      // minimum is the lane's first strict minimum: one v_min per candidate
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
           const_cast<int32_t*>(s2 + (int64_t)f * HW), 0, (int)(HW * 4), 0x00020000);
+      const int ry0 = 8 * by + dy0 - SR, rx0 = 8 * bx + 4 * g - SR;
+      bool vx[4];
+#pragma unroll
+      for (int s = 0; s < 4; ++s) vx[s] = 4 * g + s < N && rx0 + s >= 0 && rx0 + s + 8 <= W;
+      uint32_t best = 0xffffffffu;
 #pragma unroll
       for (int d = 0; d < DYT; ++d) {
-        const int dyi = dy0 + d;
-        const int ry = 8 * by + dyi - SR, rx0 = 8 * bx + 4 * g - SR;
-        const bool vy = dyi < N && ry >= 0 && ry + 8 <= H;
+        const int ry = ry0 + d;
+        const bool vy = dy0 + d < N && ry >= 0 && ry + 8 <= H;
         // rx0 is a multiple of 4, so rx0 < 0 means all four candidates are off-frame
         const me_u32x4 sq = __builtin_amdgcn_raw_buffer_load_b128(
             rs, vy && rx0 >= 0 ? (ry * W + rx0) * 4 : 0x40000000, 0, 0);
         const uint32_t sv[4] = {sq.x, sq.y, sq.z, sq.w};
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          const int dxi = 4 * g + s;
-          const int rx = rx0 + s;
-          const bool valid = vy && dxi < N && rx >= 0 && rx + 8 <= W;
-          const int k = (int)sv[s] - 2 * (int)acc[d][s];
-          const bool better = valid && k < bestk;
-          bestk = better ? k : bestk;
-          besti = better ? dyi * N + dxi : besti;
+          const uint32_t key = (sv[s] << 5) + ((1u << 27) + 4u * d + s) - (acc[d][s] << 6);
+          best = vy && vx[s] ? min(best, key) : best;
         }
+      }
+      if (best != 0xffffffffu) {
+        bestk = (int)(best >> 5);                          // K + 2^22 (same bias on every lane)
+        const int r = (int)(best & 31u);
+        besti = (dy0 + (r >> 2)) * N + 4 * g + (r & 3);
       }
     }
     // lexicographic (K, index) minimum over the block's aligned lane segment; lanes with no
