@@ -327,7 +327,8 @@ struct FusedArgs {
   uint32_t nframes;      // number of output frames F
   int H, W, h, w, tpr;   // tpr = tiles (of 8 blocks) per block row
   int sr;
-  int dup12;             // table planes 1 and 2 identical (always true for PatchQuant tables)
+  int dup12;             // table planes 1 and 2 identical (always true for PatchQuant tables);
+                         // C = 1 kernels take it as the template flag DUP
 #ifdef IVC_ABLATION
   int ablate;            // diagnostic builds only (tools/ablate): bit mask of skipped phases
 #endif
@@ -350,13 +351,16 @@ struct FusedArgs {
 #endif
 
 constexpr int XS_PITCH = 72;   // T elements per block in the transpose image
-constexpr int OS_PITCH = 200;  // int32 per block in the output staging (192 + 8 pad)
+// int32 per block in the output staging: 3 planes (192 + 8 pad), or 2 planes (128 + 8) when
+// a C = 1 input's planes 1 and 2 are equal (DUP: plane 1 is stored twice)
+template <int C, bool DUP>
+constexpr int os_pitch() { return C == 1 && DUP ? 136 : 200; }
 constexpr int OOB = 0x40000000;  // buffer offset beyond every descriptor range used here
 
-template <typename T, int C>
+template <typename T, int C, bool DUP>
 struct WaveLds {
   static constexpr int XS = 8 * XS_PITCH * (int)sizeof(T);
-  static constexpr int OS = 8 * OS_PITCH * 4;
+  static constexpr int OS = 8 * os_pitch<C, DUP>() * 4;
   static constexpr int BYTES = C == 1 ? (XS > OS ? XS : OS) : XS + OS;  // C = 1 aliases them
 };
 
@@ -516,9 +520,10 @@ __device__ __forceinline__ void gather_inter(const FusedArgs& a, uint32_t lt, in
 
 // The staged group (LDS, block pitch OS_PITCH) leaves as 6 x 1 KiB buffer_store_dwordx4;
 // lanes past a ragged group's edge, or a non-existent group, fall outside the descriptor.
-template <int NG>
+template <int NG, int C, bool DUP>
 __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* os, int lane,
                                             uint32_t lt, int g, bool exists) {
+  constexpr int PITCH = os_pitch<C, DUP>();
   const GroupLoc L = group_loc<NG>(a, lt, g);
   const __amdgpu_buffer_rsrc_t ro =
       make_rsrc(a.out + (((int64_t)L.f * a.h + L.bi) * a.w + L.bj0) * 192,
@@ -527,16 +532,19 @@ __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* o
   for (int jj = 0; jj < 6; ++jj) {
     const int ch = lane + 64 * jj;
     const int bb = ch / 48;
-    const int4 val = *reinterpret_cast<const int4*>(os + bb * OS_PITCH + (ch - bb * 48) * 4);
+    int cc = ch - bb * 48;                               // 16-byte chunk inside the block
+    if (C == 1 && DUP && cc >= 32) cc -= 16;             // plane 2 = staged plane 1
+    const int4 val = *reinterpret_cast<const int4*>(os + bb * PITCH + cc * 4);
     const u32x4 w4 = {(uint32_t)val.x, (uint32_t)val.y, (uint32_t)val.z, (uint32_t)val.w};
     __builtin_amdgcn_raw_buffer_store_b128(w4, ro, ch * 16, 0, IVC_STORE_AUX);
   }
 }
 
 // Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging.
-template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG>
+template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
+          bool DUP>
 __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI, C, SRC>& v,
-                                             T* xs, int32_t* os, const double2* srq, const D* sq,
+                                             T* xs, int32_t* os, const double* srq, const D* sq,
                                              int b, int r, uint32_t zp0, uint32_t zp1) {
 #pragma unroll
   for (int c = 0; c < C; ++c) {
@@ -586,50 +594,46 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
     // ---- quantise ---------------------------------------------------------------------------
 #pragma unroll
     for (int pi = 0; pi < (C == 1 ? 3 : 1); ++pi) {
-      if (C == 1 && pi == 2 && a.dup12) break;  // plane 2 == plane 1: written with plane 1
+      if (C == 1 && DUP && pi == 2) break;  // plane 2 == plane 1: stored from plane 1
       const int p = C == 1 ? pi : c;
-      int qv[8];
+      int32_t* ob = os + b * os_pitch<C, DUP>() + p * 64;
+      auto pos_of = [&](int i) {
+        return ZZ ? (int)(((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u) : i * 8 + r;
+      };
       if (IVC_SKIP(a, 4)) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) qv[i] = (int)x[i];
+        for (int i = 0; i < 8; ++i) ob[pos_of(i)] = (int)x[i];
       } else if constexpr (FAST) {
+        // quotient via the scaled reciprocal, staged at once; values within 2^-30 of a
+        // rounding boundary (or too large to bound the error) are redone below by exact
+        // IEEE division (rare; one wave-uniform test)
         bool all_ok = true;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-          const double2 e = srq[p * 64 + i * 8 + r];
-          const double yq = x[i] * e.x;
+          const double yq = x[i] * srq[p * 64 + i * 8 + r];
           const double rr = __builtin_rint(yq);
-          bool ok = __builtin_fabs(yq - rr) < e.y;
+          bool ok = __builtin_fabs(yq - rr) < 0.5 - 0x1p-30;
           if (CHECKMAG) ok = ok && __builtin_fabs(yq) < 0x1p20;
           all_ok = all_ok && ok;
-          qv[i] = (int)rr;
+          ob[pos_of(i)] = (int)rr;
         }
-        // exact IEEE division next to a rounding boundary (rare; one wave-uniform test)
         if (__ballot(!all_ok)) {
 #pragma unroll
           for (int i = 0; i < 8; ++i) {
-            const double2 e = srq[p * 64 + i * 8 + r];
-            const double yq = x[i] * e.x;
+            const double yq = x[i] * srq[p * 64 + i * 8 + r];
             const double rr = __builtin_rint(yq);
-            bool ok = __builtin_fabs(yq - rr) < e.y;
+            bool ok = __builtin_fabs(yq - rr) < 0.5 - 0x1p-30;
             if (CHECKMAG) ok = ok && __builtin_fabs(yq) < 0x1p20;
             if (!ok) {
               const double Y = x[i] * (dct2_scale(i) * dct2_scale(r));
-              qv[i] = np_to_i32<double>(__builtin_rint(Y / (double)sq[p * 64 + i * 8 + r]));
+              ob[pos_of(i)] = np_to_i32<double>(__builtin_rint(Y / (double)sq[p * 64 + i * 8 + r]));
             }
           }
         }
       } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          qv[i] = np_to_i32<D>(rint_t<D>((D)x[i] / sq[p * 64 + i * 8 + r]));
-      }
-      int32_t* ob = os + b * OS_PITCH + p * 64;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int pos = ZZ ? (int)(((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u) : i * 8 + r;
-        ob[pos] = qv[i];
-        if (C == 1 && pi == 1 && a.dup12) ob[64 + pos] = qv[i];
+          ob[pos_of(i)] = np_to_i32<D>(rint_t<D>((D)x[i] / sq[p * 64 + i * 8 + r]));
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -637,28 +641,20 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
 }
 
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
-          int NG>
+          int NG, bool DUP>
 __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) {
-  typedef WaveLds<T, C> L;
+  typedef WaveLds<T, C, DUP> L;
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
-  __shared__ double2 srq[FAST ? 192 : 1];
+  __shared__ double srq[FAST ? 192 : 1];
   __shared__ D sq[192];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   const int b = lane >> 3, r = lane & 7;
   for (int i = tid; i < 192; i += 256) {
     sq[i] = (D)t.q[i];
-    // {s_i * s_k * RN(1/q), rounding-boundary threshold}: for a power-of-two q the
-    // reciprocal product IS the exact quotient, so its threshold (> 0.5) never sends it to
-    // the division.  1.0 / q is IEEE-correctly rounded here as on the host.
-    if constexpr (FAST) {
-      const double q = t.q[i];
-      const double rq = (dct2_scale((i >> 3) & 7) * dct2_scale(i & 7)) * (1.0 / q);
-      const uint64_t bits = __builtin_bit_cast(uint64_t, q);
-      const uint32_t ex = (uint32_t)(bits >> 52) & 0x7ffu;
-      const bool pow2 = (bits & 0xfffffffffffffull) == 0 && ex != 0 && ex != 0x7ffu;
-      srq[i] = make_double2(rq, pow2 ? 1.0 : 0.5 - 0x1p-30);
-    }
+    // s_i * s_k * RN(1/q): the DCT's power-of-two output scales folded into the reciprocal
+    // (1.0 / q is IEEE-correctly rounded here as on the host)
+    if constexpr (FAST) srq[i] = (dct2_scale((i >> 3) & 7) * dct2_scale(i & 7)) * (1.0 / t.q[i]);
   }
   // zig-zag positions of this lane's column (raster i*8 + r), packed 4 per register
   uint32_t zp0 = 0, zp1 = 0;
@@ -686,7 +682,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
   if constexpr (SRC == SRC_IMAGE) {
     load_tile<TI, C, NG>(a, lt, lt < nlt, lane, raw);
 #pragma unroll
-    for (int g = 1; g < NG; ++g) store_group<NG>(a, os, lane, 0u, 0, false);
+    for (int g = 1; g < NG; ++g) store_group<NG, C, DUP>(a, os, lane, 0u, 0, false);
   }
   uint32_t plt = 0;
   int pg = 0;
@@ -695,7 +691,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
     TileRaw<TI, C, NG> nraw;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      store_group<NG>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+      store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
       RowReg<TI, C, SRC> v;
       if constexpr (SRC == SRC_IMAGE) {
         if (g == 0) {
@@ -706,41 +702,44 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
       } else {
         gather_inter(a, lt, b, r, v);
       }
-      encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+      encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
       plt = lt;
       pg = g;
       have_prev = true;
     }
     if constexpr (SRC == SRC_IMAGE) raw = nraw;
   }
-  store_group<NG>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+  store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
 }
 
 
-// Persistent grids: exactly the resident workgroup count (occupancy query, cached per
-// kernel), so no workgroup starts after the first wave of workgroups has drained — a grid
-// above residency runs its surplus as a second, partially occupied wave.
 static std::mutex g_occ_mu;
 static std::unordered_map<const void*, int> g_occ;
 
-template <typename K>
-static unsigned resident_grid(K kernel, int64_t work_groups_needed) {
+// Persistent grids: as many 256-thread groups as the device holds at once (occupancy of
+// this kernel, cached per kernel), never more than the work needs.
+unsigned resident_grid_ptr(const void* kernel, int64_t work_groups_needed) {
   int per_cu = 0;
   {
     std::lock_guard<std::mutex> g(g_occ_mu);
-    auto it = g_occ.find((const void*)kernel);
+    auto it = g_occ.find(kernel);
     if (it != g_occ.end()) {
       per_cu = it->second;
     } else {
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, 256, 0) != hipSuccess ||
           per_cu < 1)
         per_cu = 1;
-      g_occ[(const void*)kernel] = per_cu;
+      g_occ[kernel] = per_cu;
     }
   }
   int64_t g = (int64_t)num_cus() * per_cu;
   if (work_groups_needed < g) g = work_groups_needed;
   return (unsigned)(g < 1 ? 1 : g);
+}
+
+template <typename K>
+static unsigned resident_grid(K kernel, int64_t work_groups_needed) {
+  return resident_grid_ptr(reinterpret_cast<const void*>(kernel), work_groups_needed);
 }
 
 // NG: groups of 8 blocks per wave load (wide, whole-cache-line row loads for u8 luma)
@@ -751,8 +750,13 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
   FusedArgs a = a_in;
   a.tpr = (a.w + 8 * NG - 1) / (8 * NG);
   const int64_t nlt = (int64_t)a.nframes * a.h * a.tpr;
-  auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG>;
-  k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
+  if (C == 1 && a.dup12) {
+    auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, C == 1>;
+    k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
+  } else {
+    auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, false>;
+    k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
+  }
 }
 
 // The FAST quotient check needs |quotient| < 2^20.  Integer pixels

@@ -260,6 +260,11 @@ __global__ __launch_bounds__(256) void me_s2_kernel(const uint8_t* __restrict__ 
   }
 }
 
+static unsigned me_fast_grid(const void* kernel, int64_t wgs) {
+  const int64_t g = 2 * (int64_t)resident_grid_ptr(kernel, wgs);
+  return (unsigned)(g < wgs ? g : wgs);
+}
+
 template <int SR> struct MeCfg;
 // PITCH: LDS row pitch of a staged window (dwords), chosen so a row read of a 32-lane half
 // hits distinct banks (searched offline; SR = 4 is 2-way at best with 4 blocks per wave)
@@ -501,15 +506,20 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
       if (!s2) return hipErrorOutOfMemory;
       me_s2_kernel<<<me_grid(nframes * ((W - 8) / 4 + 1) * ((H - 8) / S2Y + 1), 256, 8), 256, 0, s>>>(
           (const uint8_t*)ref, nframes, h, w, s2);
+      // persistent (group stride = all waves), launched at 2x what fits at once: the waves of
+      // the second residency round fill the SIMDs as the first ones drain (measured faster
+      // than an exactly resident grid, the kernel being VALU-throughput bound)
       const int64_t groups_bpw1 = nframes * (H / 8) * (W / 8);
+#define ME_FAST(R, BPW)                                                                       \
+  me_fast_u8_kernel<R><<<me_fast_grid(reinterpret_cast<const void*>(me_fast_u8_kernel<R>),      \
+                                      ((groups_bpw1 + BPW - 1) / BPW + 3) / 4),                 \
+                         256, 0, s>>>((const uint8_t*)ref, (const uint8_t*)cur, s2, nframes, h, w, mv)
       switch (sr) {
-        case 4: me_fast_u8_kernel<4><<<me_grid((groups_bpw1 / 4 + 3) / 4, 1, 8), 256, 0, s>>>(
-                    (const uint8_t*)ref, (const uint8_t*)cur, s2, nframes, h, w, mv); break;
-        case 8: me_fast_u8_kernel<8><<<me_grid((groups_bpw1 / 2 + 3) / 4, 1, 8), 256, 0, s>>>(
-                    (const uint8_t*)ref, (const uint8_t*)cur, s2, nframes, h, w, mv); break;
-        default: me_fast_u8_kernel<16><<<me_grid((groups_bpw1 + 3) / 4, 1, 8), 256, 0, s>>>(
-                    (const uint8_t*)ref, (const uint8_t*)cur, s2, nframes, h, w, mv); break;
+        case 4: ME_FAST(4, 4); break;
+        case 8: ME_FAST(8, 2); break;
+        default: ME_FAST(16, 1); break;
       }
+#undef ME_FAST
       return hipGetLastError();
     }
     switch (sr) {

@@ -306,6 +306,27 @@ def test_intra_encode_vs_oracle(scale, dtype):
         assert_bits(out[f], O.intra_encode(img[f], scale, zigzag=True), f"frame {f}")
 
 
+@pytest.mark.parametrize("dtype", [np.uint8, np.float64])
+@pytest.mark.parametrize("zz", [0, 1])
+def test_intra_encode_distinct_chroma_planes(dtype, zz):
+    """A C-ABI table whose planes 1 and 2 differ (PatchQuant never builds one): the C = 1
+    kernels then stage and quantise all three planes instead of storing plane 1 twice."""
+    N, L = _native()
+    rng = np.random.default_rng(12)
+    F, H, W = 2, 48, 136
+    img = (rng.integers(0, 256, (F, H, W, 1), dtype=np.uint8) if dtype == np.uint8
+           else rng.normal(128, 60, (F, H, W, 1)))
+    table = PatchQuant(0.5).get_quantization_table().astype(np.float64)
+    table[2] *= 1.37
+    out = np.empty((F, H // 8, W // 8, 3, 64), np.int32)
+    N.check(L.ivc_intra_encode(N.ptr(img), N.DTYPE_CODE[np.dtype(dtype)], F, H, W, 1,
+                               N.ptr(N.table_arg(table)), N.F64, zz, N.ptr(out)))
+    for f in range(F):
+        want = np.round(O.dct_transform(O.patch(img[f])) / table[None, None]).astype(np.int32)
+        want = O.zigzag_flatten(want) if zz else want.reshape(H // 8, W // 8, 3, 64)
+        assert_bits(out[f], want, f"frame {f}")
+
+
 def test_intra_encode_4k_full_frame():
     """One full cfg3 frame (3840x2160 luma) bit-exact against the oracle."""
     N, L = _native()
