@@ -81,9 +81,11 @@ def intra_frames(F, H, W, seed, dev):
     return out
 
 
-def inter_frames(F, H, W, seed, dev):
-    """Smooth base texture shifted by (dy, dx) = ((f % 7) - 3, (2f % 9) - 4) plus +-2 noise
-    (SURVEY §8d cfg4), so consecutive frames differ by a motion within +-16."""
+def inter_frames(F, H, W, seed, dev, first=0):
+    """Frames first .. first+F-1 of a sequence: a smooth base texture shifted by
+    (dy, dx) = ((f % 7) - 3, (2f % 9) - 4) plus +-2 noise, so consecutive
+    frames differ by a motion within +-16.  Frame f depends only on (seed, f), so ranks
+    generating disjoint frame ranges of one sequence agree on the shared halo frame."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     P = 16
@@ -93,11 +95,14 @@ def inter_frames(F, H, W, seed, dev):
     base = base[0, 0, :H + 2 * P, :W + 2 * P]
     base = base + torch.randint(-12, 13, base.shape, device=dev, generator=g).float()
     out = torch.empty((F, H, W), dtype=torch.uint8, device=dev)
-    for f in range(F):
+    for i in range(F):
+        f = first + i
+        gf = torch.Generator(device=dev)
+        gf.manual_seed(seed * 1000003 + f)
         dy, dx = (f % 7) - 3, (2 * f % 9) - 4
         fr = base[P + dy:P + dy + H, P + dx:P + dx + W]
-        fr = fr + torch.randint(-2, 3, (H, W), device=dev, generator=g).float()
-        out[f] = fr.round().clamp(0, 255).to(torch.uint8)
+        fr = fr + torch.randint(-2, 3, (H, W), device=dev, generator=gf).float()
+        out[i] = fr.round().clamp(0, 255).to(torch.uint8)
     return out
 
 
@@ -183,6 +188,9 @@ def main():
     ap.add_argument("--no-inter", action="store_true")
     ap.add_argument("--no-intra", action="store_true", help="profiling aid: skip the cfg3 leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the cfg5 8K leg")
+    ap.add_argument("--sharded-frames", type=int, default=120)
+    ap.add_argument("--sharded-steps", type=int, default=3)
     args = ap.parse_args()
 
     dist, rank, world, local = dist_setup(args.gpus)
@@ -287,6 +295,50 @@ def main():
                           f"of a 1080p pair at sr={sr}; {per_cand * 1e6:.3f} us per valid candidate, "
                           "extrapolated by exact valid-candidate count"}
         del seq, mv, q
+        torch.cuda.empty_cache()
+
+    # ---- cfg5: 8K x 120 frames, frame-sharded ME + DCT, one all-gather of histograms ------
+    if not args.no_sharded:
+        from ivclab_amd.distributed import shard_pairs
+        F5, H5, W5, sr5 = args.sharded_frames, 4320, 7680, 16
+        a5, b5 = shard_pairs(F5, rank, world)          # this rank's frames incl. the halo
+        n5 = max(b5 - a5, 0)
+        seq5 = inter_frames(max(n5, 2), H5, W5, seed=5, dev=dev, first=a5)[:n5]
+        pairs5 = max(n5 - 1, 0)
+        mv5 = torch.empty((max(pairs5, 1), H5 // 8, W5 // 8), dtype=torch.int64, device=dev)
+        q5 = torch.empty((max(pairs5, 1), H5 // 8, W5 // 8, 3, 64), dtype=torch.int32, device=dev)
+        nmv = (2 * sr5 + 1) ** 2
+        hist5 = torch.zeros(HIST_BINS + nmv, dtype=torch.int64, device=dev)
+
+        def sstep():
+            # the step: ME + MC + residual DCT + quantise of this rank's pairs, then the
+            # symbol histograms (coefficients | MV indices) and their all-gather
+            hist5.zero_()
+            if pairs5:
+                D.inter_encode(seq5, sr5, table, mv5, q5, zigzag=args.zigzag)
+                D.histogram(q5.view(-1), HIST_LO, hist5[:HIST_BINS])
+                D.histogram(mv5.view(-1), 0, hist5[HIST_BINS:])
+            return global_histogram(hist5)
+
+        swall, _ = timed(dist, sstep, args.sharded_steps, 1)
+        g5 = sstep()
+        total5 = (F5 - 1) * H5 * W5
+        result["sharded"] = {
+            "metric": "Mpixels/s: 8K frame-sharded +-16 ME + residual DCT+quant with one "
+                      "histogram all-gather (cfg5)",
+            "value": round(total5 * args.sharded_steps / swall / 1e6, 1), "unit": "Mpixels/s",
+            "scaling": "strong",
+            "ms_per_step": round(swall / args.sharded_steps * 1e3, 3),
+            "config": {"workload": f"cfg5: {F5} frames {W5}x{H5} u8 luma split across {world} "
+                                   f"rank(s) (+1 halo frame each), sr={sr5}",
+                       "pairs_per_rank_max": int(max_over_ranks(dist, float(pairs5)))},
+            "exchange": {"collective": "all_gather_into_tensor (RCCL)" if dist is not None
+                         else "none (1 rank)",
+                         "bins": HIST_BINS + nmv,
+                         "symbols": int(g5[:HIST_BINS].sum().item()),
+                         "motion_vectors": int(g5[HIST_BINS:].sum().item())},
+        }
+        del seq5, mv5, q5
         torch.cuda.empty_cache()
 
     if rank == 0 and not args.no_cpu:

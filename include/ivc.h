@@ -161,6 +161,12 @@ int ivc_inter_encode_dev(const uint8_t* frames, int64_t nframes, int64_t H, int6
 int ivc_histogram_i32(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, int64_t* hist);
 int ivc_histogram_i32_dev(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins,
                           int64_t* hist, void* stream);
+/* The same over int64 symbols: the motion-vector indices of ivc_motion_estimate /
+ * ivc_inter_encode_dev ((2 sr + 1)^2 bins for VideoCodec's motion Huffman table,
+ * ivclab/video/videocodec.py:33,62).                                                       */
+int ivc_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist);
+int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
+                          int64_t* hist, void* stream);
 
 #ifdef __cplusplus
 }

@@ -61,6 +61,8 @@ _SIGS = {
     "ivc_inter_encode_dev": ([_P, _L, _L, _L, _I, _P, _I, _I, _P, _P, _P], _I),
     "ivc_histogram_i32": ([_P, _L, _ct.c_int32, _ct.c_int32, _P], _I),
     "ivc_histogram_i32_dev": ([_P, _L, _ct.c_int32, _ct.c_int32, _P, _P], _I),
+    "ivc_histogram_i64": ([_P, _L, _L, _ct.c_int32, _P], _I),
+    "ivc_histogram_i64_dev": ([_P, _L, _L, _ct.c_int32, _P, _P], _I),
 }
 EXPORTS = tuple(_SIGS)
 

@@ -489,4 +489,25 @@ int ivc_histogram_i32(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, 
   return st.sync();
 }
 
+int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist,
+                          void* stream) {
+  CHECK(n >= 0 && nbins > 0, IVC_E_ARG, "histogram: need n >= 0 and nbins > 0");
+  return dev_launch(launch_histogram_i64(sym, n, lo, nbins, hist, (hipStream_t)stream),
+                    "histogram");
+}
+
+int ivc_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist) {
+  CHECK(n >= 0 && nbins > 0, IVC_E_ARG, "histogram: need n >= 0 and nbins > 0");
+  Staging st;
+  TRY(st.open());
+  const size_t hb = (size_t)nbins * 8;
+  void* d_sym = st.in(sym, (size_t)n * 8);
+  int64_t* d_hist = (int64_t*)st.in(hist, hb);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_histogram_i64((const int64_t*)d_sym, n, lo, nbins, d_hist,
+                                       st.ctx->stream), "histogram"));
+  TRY(st.out(hist, d_hist, hb));
+  return st.sync();
+}
+
 }  // extern "C"

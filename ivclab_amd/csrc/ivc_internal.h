@@ -39,6 +39,8 @@ hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int6
 hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, int unzigzag,
                                double* out, hipStream_t s);
 unsigned resident_grid_ptr(const void* kernel, int64_t work_groups_needed);
+hipError_t launch_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
+                                int64_t* hist, hipStream_t s);
 hipError_t launch_histogram(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins,
                             int64_t* hist, hipStream_t s);
 

@@ -341,10 +341,16 @@ struct FusedArgs {
 // cache-policy bits of the streamed output stores / input loads (diagnostic builds may
 // override them with -D to compare policies)
 #ifndef IVC_STORE_AUX
-#define IVC_STORE_AUX 0
+#define IVC_STORE_AUX 2   // nt: streamed output (measured +0.8% on the cfg3 bench)
 #endif
 #ifndef IVC_LOAD_AUX
 #define IVC_LOAD_AUX 0
+#endif
+#ifndef IVC_FUSED_WGCU
+#define IVC_FUSED_WGCU 0   // > 0: at most this many workgroups per CU (diagnostic builds)
+#endif
+#ifndef IVC_FUSED_GRID
+#define IVC_FUSED_GRID 0
 #endif
 #ifndef IVC_WIDE_NG
 #define IVC_WIDE_NG 2    // u8 luma: 8 rows x 128 bytes per wave load (whole cache lines)
@@ -750,12 +756,23 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
   FusedArgs a = a_in;
   a.tpr = (a.w + 8 * NG - 1) / (8 * NG);
   const int64_t nlt = (int64_t)a.nframes * a.h * a.tpr;
+  // IVC_FUSED_GRID: 0 = exactly resident (persistent waves), k > 0 = k tiles per wave
+  auto grid = [&](auto k) -> unsigned {
+    if (IVC_FUSED_GRID == 0) {
+      unsigned g = resident_grid(k, (nlt + 3) / 4);
+      if (IVC_FUSED_WGCU > 0 && g > (unsigned)(num_cus() * IVC_FUSED_WGCU))
+        g = (unsigned)(num_cus() * IVC_FUSED_WGCU);
+      return g;
+    }
+    const int64_t g = (nlt + 4 * IVC_FUSED_GRID - 1) / (4 * IVC_FUSED_GRID);
+    return (unsigned)(g < 1 ? 1 : g);
+  };
   if (C == 1 && a.dup12) {
     auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, C == 1>;
-    k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
+    k<<<grid(k), 256, 0, s>>>(a, t);
   } else {
     auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, false>;
-    k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
+    k<<<grid(k), 256, 0, s>>>(a, t);
   }
 }
 
@@ -848,8 +865,9 @@ hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t
 // Symbol histogram (feeds stats_marg / the Huffman table, entropy.py:6-29): per-workgroup
 // LDS bins, the dominant zero symbol counted by wave ballots, one global add per bin.
 // ======================================================================================
-__global__ __launch_bounds__(256) void histogram_kernel(const int32_t* __restrict__ sym,
-                                                        int64_t n, int32_t lo, int32_t nbins,
+template <typename S>
+__global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sym, int64_t n,
+                                                        int64_t lo, int32_t nbins,
                                                         unsigned long long* __restrict__ hist,
                                                         int use_lds) {
   extern __shared__ unsigned int bins[];
@@ -858,12 +876,16 @@ __global__ __launch_bounds__(256) void histogram_kernel(const int32_t* __restric
     for (int i = tid; i < nbins; i += 256) bins[i] = 0;
     __syncthreads();
   }
-  const int64_t zb64 = (int64_t)0 - lo;
-  const int zb = zb64 < 0 ? 0 : (zb64 >= nbins ? nbins - 1 : (int)zb64);
+  // the bin of symbol value 0 (the dominant symbol) is counted per thread, added once
+  const uint64_t nlo = (uint64_t)0 - (uint64_t)lo;   // -lo without overflow
+  const int zb = lo > 0 ? 0 : (nlo >= (uint64_t)nbins ? nbins - 1 : (int)nlo);
   unsigned zeros = 0;
-  auto count = [&](int32_t v) {
-    const int64_t b64 = (int64_t)v - lo;
-    const int b = b64 < 0 ? 0 : (b64 >= nbins ? nbins - 1 : (int)b64);
+  auto count = [&](S v) {
+    // clamp into the end bins; v - lo is formed unsigned once v > lo (no overflow)
+    int b;
+    if ((int64_t)v <= lo) b = 0;
+    else if ((uint64_t)(int64_t)v - (uint64_t)lo >= (uint64_t)nbins) b = nbins - 1;
+    else b = (int)((uint64_t)(int64_t)v - (uint64_t)lo);
     if (b == zb) {
       ++zeros;
     } else if (use_lds) {
@@ -872,46 +894,61 @@ __global__ __launch_bounds__(256) void histogram_kernel(const int32_t* __restric
       atomicAdd(&hist[b], 1ull);
     }
   };
-  // 16 B per lane, two loads in flight per iteration (the symbol stream is read once)
-  // a 4-byte-aligned stream that does not start on 16 B: the first `head` symbols apart
-  int64_t head = (int64_t)((16u - ((uintptr_t)sym & 15u)) & 15u) >> 2;
+  // a stream that does not start on 16 B: the first `head` symbols apart
+  constexpr int PER = 16 / (int)sizeof(S);
+  int64_t head = (int64_t)(((16u - ((uintptr_t)sym & 15u)) & 15u) / sizeof(S));
   if (head > n) head = n;
   if (blockIdx.x == 0 && tid < head) count(sym[tid]);
   sym += head;
   n -= head;
-  typedef int hi4 __attribute__((ext_vector_type(4)));
-  const hi4* s4 = reinterpret_cast<const hi4*>(sym);
-  const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * 256;
+  // 16 B per lane, two loads in flight per iteration (the symbol stream is read once)
+  typedef S vec_t __attribute__((ext_vector_type(PER)));
+  const vec_t* sv = reinterpret_cast<const vec_t*>(sym);
+  const int64_t nv = n / PER, stride = (int64_t)gridDim.x * 256;
   int64_t i = (int64_t)blockIdx.x * 256 + tid;
-  for (; i + stride < n4; i += 2 * stride) {
-    const hi4 a = __builtin_nontemporal_load(s4 + i);
-    const hi4 b = __builtin_nontemporal_load(s4 + i + stride);
-    count(a.x); count(a.y); count(a.z); count(a.w);
-    count(b.x); count(b.y); count(b.z); count(b.w);
+  for (; i + stride < nv; i += 2 * stride) {
+    const vec_t a = __builtin_nontemporal_load(sv + i);
+    const vec_t b = __builtin_nontemporal_load(sv + i + stride);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) count(a[k]);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) count(b[k]);
   }
-  if (i < n4) {
-    const hi4 a = __builtin_nontemporal_load(s4 + i);
-    count(a.x); count(a.y); count(a.z); count(a.w);
+  if (i < nv) {
+    const vec_t a = __builtin_nontemporal_load(sv + i);
+#pragma unroll
+    for (int k = 0; k < PER; ++k) count(a[k]);
   }
-  if (blockIdx.x == 0 && tid < (int)(n & 3)) count(sym[(n4 << 2) + tid]);
+  if (blockIdx.x == 0 && tid < (int)(n - nv * PER)) count(sym[nv * PER + tid]);
   if (use_lds) {
     atomicAdd(&bins[zb], zeros);
     __syncthreads();
-    for (int i = tid; i < nbins; i += 256)
-      if (bins[i]) atomicAdd(&hist[i], (unsigned long long)bins[i]);
+    for (int i2 = tid; i2 < nbins; i2 += 256)
+      if (bins[i2]) atomicAdd(&hist[i2], (unsigned long long)bins[i2]);
   } else if (zeros) {
     atomicAdd(&hist[zb], (unsigned long long)zeros);
   }
 }
 
-hipError_t launch_histogram(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins,
-                            int64_t* hist, hipStream_t s) {
+template <typename S>
+static hipError_t launch_hist(const S* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist,
+                              hipStream_t s) {
   if (n <= 0 || nbins <= 0) return hipSuccess;
   const int use_lds = nbins <= 16384;
   const size_t lds = use_lds ? (size_t)nbins * 4 : 0;
-  histogram_kernel<<<grid_for(n, 256 * 16, 4), 256, lds, s>>>(
+  histogram_kernel<S><<<grid_for(n, 256 * 16, 4), 256, lds, s>>>(
       sym, n, lo, nbins, reinterpret_cast<unsigned long long*>(hist), use_lds);
   return hipGetLastError();
+}
+
+hipError_t launch_histogram(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins,
+                            int64_t* hist, hipStream_t s) {
+  return launch_hist<int32_t>(sym, n, lo, nbins, hist, s);
+}
+
+hipError_t launch_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
+                                int64_t* hist, hipStream_t s) {
+  return launch_hist<int64_t>(sym, n, lo, nbins, hist, s);
 }
 
 }  // namespace ivc

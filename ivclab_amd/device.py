@@ -80,7 +80,17 @@ def motion_estimate(ref, cur, sr, mv, exact_u8=False, stream=None):
 
 
 def histogram(sym, lo, hist, stream=None):
-    """hist[v - lo] += 1 over the int32 tensor sym (clamped into the end bins)."""
+    """hist[v - lo] += 1 over the int32 or int64 tensor sym (clamped into the end bins);
+    hist is an int64 tensor of nbins counts (accumulated onto)."""
+    import torch
     _contig(sym, "sym"); _contig(hist, "hist")
-    N.check(N.lib().ivc_histogram_i32_dev(sym.data_ptr(), sym.numel(), int(lo), hist.numel(),
-                                          hist.data_ptr(), _stream(stream)), "histogram")
+    if hist.dtype != torch.int64:
+        raise ValueError("histogram: hist must be int64")
+    if sym.dtype == torch.int32:
+        fn = N.lib().ivc_histogram_i32_dev
+    elif sym.dtype == torch.int64:
+        fn = N.lib().ivc_histogram_i64_dev
+    else:
+        raise ValueError(f"histogram: symbols must be int32 or int64, got {sym.dtype}")
+    N.check(fn(sym.data_ptr(), sym.numel(), int(lo), hist.numel(), hist.data_ptr(),
+               _stream(stream)), "histogram")

@@ -351,13 +351,28 @@ def test_histogram_vs_oracle():
         assert np.array_equal(h, O.histogram(sym, lo, nb))
 
 
-def test_histogram_device_offsets_and_ragged():
-    """Device histogram on views that start off 16 B and lengths that are not multiples of 4
-    (the kernel reads 16 B per lane after an unaligned head)."""
+def test_histogram_i64_vs_oracle():
+    """int64 symbols (motion-vector indices): host entry point, values beyond both ends."""
+    N, L = _native()
+    rng = np.random.default_rng(3)
+    sym = rng.integers(-50, 1200, (1 << 18) + 5).astype(np.int64)
+    sym[::7] = 0
+    sym[:4] = [-(1 << 62), 1 << 62, np.iinfo(np.int64).min + 1, np.iinfo(np.int64).max]
+    for lo, nb in ((0, 1089), (-64, 2048), (-40000, 70000)):
+        h = np.zeros(nb, np.int64)
+        N.check(L.ivc_histogram_i64(N.ptr(sym), sym.size, lo, nb, N.ptr(h)))
+        want = O.histogram(np.clip(sym, lo - 1, lo + nb + 1), lo, nb)
+        assert np.array_equal(h, want), (lo, nb)
+
+
+@pytest.mark.parametrize("dt", ["int32", "int64"])
+def test_histogram_device_offsets_and_ragged(dt):
+    """Device histogram on views that start off 16 B and lengths that are not multiples of
+    the 16-byte vector (the kernel reads 16 B per lane after an unaligned head)."""
     torch = pytest.importorskip("torch")
     import ivclab_amd.device as D
     rng = np.random.default_rng(2)
-    base = rng.integers(-300, 300, (1 << 16) + 9).astype(np.int32)
+    base = rng.integers(-300, 300, (1 << 16) + 9).astype(dt)
     base[::5] = 0
     t = torch.from_numpy(base).cuda()
     for off in (0, 1, 2, 3):

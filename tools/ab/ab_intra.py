@@ -53,19 +53,30 @@ def timeit(fn):
 
 F, H, W = args.frames, 2160, 3840
 img = bench.intra_frames(F, H, W, seed=3, dev=dev)
-outs = [torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev) for _ in libs]
+# one output buffer for every variant (separate buffers showed placement-dependent timings);
+# the first variant's output is kept as the reference
+o = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+ref, same = None, {}
 res = {n: [] for n, _ in libs}
-for _ in range(args.rounds):
-    for (n, L), o in zip(libs, outs):
+fill = []
+for rnd in range(args.rounds):
+    fill.append(timeit(lambda: o.fill_(0)))
+    for n, L in libs:
         res[n].append(timeit(lambda: N.check(L.ivc_intra_encode_dev(
             img.data_ptr(), 1, F, H, W, 1, t.ctypes.data, N.F64, 0, o.data_ptr(), None, 0, 0,
             stream))))
-for (n, _), o in zip(libs, outs):
-    same = bool(torch.equal(o, outs[0]))
+        if rnd == 0:
+            if ref is None:
+                ref = o.clone()
+            same[n] = bool(torch.equal(o, ref))
+for n, _ in libs:
     med = float(np.median(res[n]))
     print(f"intra {n:24s} median {med:7.3f} ms  min {min(res[n]):7.3f}  "
-          f"{F * H * W * 13 / med / 1e6:7.1f} GB/s  same_as_first={same}", flush=True)
-del outs, img
+          f"{F * H * W * 13 / med / 1e6:7.1f} GB/s  same_as_first={same[n]}", flush=True)
+print(f"torch fill_ of the same output buffer: median {float(np.median(fill)):7.3f} ms "
+      f"({o.numel() * 4 / float(np.median(fill)) / 1e6:7.1f} GB/s)", flush=True)
+del o, ref
+del img
 torch.cuda.empty_cache()
 
 if args.inter:

@@ -34,13 +34,31 @@ out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
 from ivclab_amd import PatchQuant  # noqa: E402
 t = N.table_arg(PatchQuant(1.0).get_quantization_table())
 modes = {}
-for ng in (1, 2, 4, 8):
+for ng in [int(x) for x in os.environ.get("ABL_NG", "1,2,4,8").split(",")]:
     modes[f"ng{ng} full"] = (0, ng)
     modes[f"ng{ng} mem-only"] = (15, ng)
     modes[f"ng{ng} no-load"] = (32, ng)
+    modes[f"ng{ng} no-store"] = (16, ng)
+    modes[f"ng{ng} loads-only"] = (31, ng)
+    modes[f"ng{ng} stores-only"] = (47, ng)
 res = {k: [] for k in modes}
+res["torch fill_ (same buffer)"] = []
 ms = ctypes.c_float()
+
+
+def fill_ms():
+    s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    out.fill_(0)
+    s_.record()
+    for _ in range(3):
+        out.fill_(0)
+    e_.record()
+    torch.cuda.synchronize()
+    return s_.elapsed_time(e_) / 3
+
+
 for rnd in range(5):
+    res["torch fill_ (same buffer)"].append(fill_ms())
     for k, (m, ng) in modes.items():
         rc = L.diag_intra_u8(img.data_ptr(), F, H, W, t.ctypes.data, out.data_ptr(), m, ng, 3, ctypes.byref(ms))
         assert rc == 0, rc
@@ -48,4 +66,5 @@ for rnd in range(5):
 bytes_ = F * H * W * 13
 for k, v in res.items():
     med = float(np.median(v))
-    print(f"{k:22s} median {med:8.3f} ms  min {min(v):8.3f}  ({bytes_ / med / 1e6:8.1f} GB/s algorithmic)")
+    print(f"{k:26s} median {med:8.3f} ms  min {min(v):8.3f}  ({bytes_ / med / 1e6:8.1f} GB/s algorithmic, "
+          f"{out.numel() * 4 / med / 1e6:8.1f} GB/s of output)")
