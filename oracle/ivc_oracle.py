@@ -235,3 +235,102 @@ def histogram(sym, lo, nbins):
     ivclab/entropy/entropy.py:6-29 bins symbols the same way with pixel_range as edges)."""
     v = np.clip(np.asarray(sym, dtype=np.int64).ravel() - lo, 0, nbins - 1)
     return np.bincount(v, minlength=nbins).astype(np.int64)
+
+
+# ---------------------------------------------------------------- zero-run coding -------
+def zerorun_encode(flat, eob=4000, block_size=64):
+    """ZeroRunCoder.encode (ivclab/entropy/zerorun.py:10-43): blocks in (h w c) order; per
+    block the coefficients up to the last nonzero one (the scan starts at block_size - 1,
+    :21-23), each nonzero value as itself and each zero run as (0, run length) (:29-37),
+    then EOB (:38); an all-zero block is just EOB (:25-27).  int32 stream."""
+    x = np.asarray(flat)
+    rows = x.reshape(-1, x.shape[-1])
+    out = []
+    for blk in rows:
+        last = block_size - 1
+        while last >= 0 and blk[last] == 0:
+            last -= 1
+        if last == -1:
+            out.append(eob)
+            continue
+        i = 0
+        while i <= last:
+            v = blk[i]
+            if v == 0:
+                run = 1
+                while i + run <= last and blk[i + run] == 0:
+                    run += 1
+                out.extend([0, run])
+                i += run
+            else:
+                out.append(int(v))
+                i += 1
+        out.append(eob)
+    return np.array(out, dtype=np.int32)
+
+
+def zerorun_encode_fast(flat, eob=4000, block_size=64):
+    """Vectorised zerorun_encode for int32 blocks of exactly block_size coefficients (same
+    stream; used for the larger parity cases)."""
+    x = np.ascontiguousarray(flat, dtype=np.int32).reshape(-1, block_size)
+    nz = x != 0
+    any_nz = nz.any(1)
+    last = np.where(any_nz, block_size - 1 - np.argmax(nz[:, ::-1], axis=1), -1)
+    pos = np.arange(block_size)
+    inside = pos[None, :] <= last[:, None]
+    prev_nz = np.concatenate([np.ones((x.shape[0], 1), bool), nz[:, :-1]], axis=1)
+    start = inside & ~nz & prev_nz                       # first zero of a run
+    # symbols per element: nonzero -> 1, run start -> 2, other zeros inside -> 0
+    per = np.where(inside & nz, 1, 0) + np.where(start, 2, 0)
+    cnt = per.sum(1) + 1                                 # + EOB
+    offs = np.concatenate([[0], np.cumsum(cnt)])
+    out = np.empty(offs[-1], np.int32)
+    within = np.cumsum(per, axis=1) - per                # exclusive position inside the block
+    base = offs[:-1, None] + within
+    r, c = np.nonzero(inside & nz)
+    out[base[r, c]] = x[r, c]
+    r, c = np.nonzero(start)
+    out[base[r, c]] = 0
+    # run length = distance to the next nonzero (which exists: the run ends before last)
+    nxt = np.where(nz, pos[None, :], block_size)
+    nxt = np.minimum.accumulate(nxt[:, ::-1], axis=1)[:, ::-1]
+    out[base[r, c] + 1] = nxt[r, c] - c
+    out[offs[1:] - 1] = eob
+    return out
+
+
+def zerorun_decode(encoded, original_shape, eob=4000, block_size=64):
+    """ZeroRunCoder.decode (ivclab/entropy/zerorun.py:46-88), including its errors:
+    ValueError on a stream that ends inside a block (:65-66), IndexError when it ends right
+    after a 0 (the run length read at :74), ValueError when a block grows past block_size
+    (:79-80) and when fewer blocks than h*w*c are found (:85-86); symbols after the last
+    expected block are ignored (:62).  Returns [h, w, c, block_size] int32."""
+    h, w, c = original_shape
+    expected = h * w * c
+    blocks = []
+    i = 0
+    n = len(encoded)
+    while i < n and len(blocks) < expected:
+        blk = []
+        while True:
+            if i >= n:
+                raise ValueError("Unexpected end of encoded symbols")
+            s = encoded[i]
+            i += 1
+            if s == eob:
+                blk.extend([0] * (block_size - len(blk)))
+                break
+            elif s == 0:
+                run = encoded[i]
+                i += 1
+                blk.extend([0] * run)
+            else:
+                blk.append(s)
+            if len(blk) > block_size:
+                raise ValueError(f"Block size exceeded: {len(blk)}")
+        if len(blk) != block_size:
+            raise ValueError(f"Incomplete block: {len(blk)}")
+        blocks.append(blk)
+    if len(blocks) != expected:
+        raise ValueError(f"Expected {expected} blocks, got {len(blocks)}")
+    return np.array(blocks, dtype=np.int32).reshape(h, w, c, block_size)

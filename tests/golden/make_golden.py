@@ -14,6 +14,8 @@ Reference modules used (paths relative to /root/reference):
   ivclab/utils/shape.py           ZigZag, Patcher
   ivclab/signal/zigzag.py         zigzag_scan
   ivclab/video/motion.py          MotionCompensator
+  ivclab/entropy/zerorun.py       ZeroRunCoder (zerorun.npz; its own RNG stream, so the
+                                  other fixtures are unchanged by its addition)
 """
 import contextlib
 import importlib.util
@@ -192,9 +194,73 @@ def main():
         p[f"zz{C}"] = _quiet(sh_m.ZigZag().flatten, qq)
         p[f"rec{C}"] = DCT.inverse_transform(Q.dequantize(_quiet(sh_m.ZigZag().unflatten, p[f"zz{C}"])))
     np.savez_compressed(os.path.join(OUT, "intra.npz"), **p)
+    make_zerorun(p)
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
+
+
+def make_zerorun(intra):
+    """ZeroRunCoder fixtures: encode streams of real zig-zag output and of adversarial
+    sparse blocks, decode round trips, and the decoder's error cases (type + message)."""
+    zr_m = _load("ivclab/entropy/zerorun.py", "ref_zerorun")
+    rng = np.random.default_rng(40)
+    z = {}
+
+    def enc(name, x, eob=4000, bs=64):
+        Z = zr_m.ZeroRunCoder(end_of_block=eob, block_size=bs)
+        z[f"{name}_x"] = x
+        z[f"{name}_eob"] = np.array(eob)
+        z[f"{name}_bs"] = np.array(bs)
+        z[f"{name}_sym"] = _quiet(Z.encode, x)
+
+    enc("zz1", intra["zz1"])
+    enc("zz3", intra["zz3"])
+    sp = rng.integers(-40, 41, (6, 7, 3, 64)).astype(np.int32)
+    sp[rng.random(sp.shape) < 0.8] = 0
+    sp[0, 0, 0] = 0                                   # all-zero block
+    sp[0, 0, 1] = 0
+    sp[0, 0, 1, 63] = -7                              # only the last coefficient
+    sp[0, 1, 0] = 0
+    sp[0, 1, 0, 0] = 3                                # only the first
+    sp[0, 1, 1] = np.where(np.arange(64) % 2 == 0, 1, 0)  # alternating
+    sp[0, 1, 2] = rng.integers(1, 9, 64)              # no zeros
+    sp[0, 2, 0] = 0
+    sp[0, 2, 0, [5, 40]] = [4000, -4000]              # a value equal to EOB
+    enc("sparse", sp)
+    enc("eob1000", sp[:2], eob=1000)
+    small = rng.integers(-3, 4, (4, 5, 1, 16)).astype(np.int32)
+    small[rng.random(small.shape) < 0.5] = 0
+    enc("bs16", small, bs=16)
+    # decode: round trips, then the error paths of zerorun.py:46-88
+    Z = zr_m.ZeroRunCoder()
+    z["dec_sparse"] = _quiet(Z.decode, z["sparse_sym"], sp.shape[:3])
+    z["dec_zz3"] = _quiet(Z.decode, z["zz3_sym"], intra["zz3"].shape[:3])
+    good = z["sparse_sym"]
+    cases = {
+        "truncated": (good[:-5], sp.shape[:3]),
+        "trailing_zero": (np.concatenate([good[:1], [0]]).astype(np.int32), (1, 1, 1)),
+        "truncated_mid": (np.array([1, 2, 0, 3], np.int32), (1, 1, 1)),
+        "ends_after_zero": (np.array([5, 0], np.int32), (1, 1, 1)),
+        "ends_after_zero2": (np.array([4000, 7, 0], np.int32), (1, 1, 2)),
+        "overflow": (np.array([0, 60, 1, 2, 3, 4, 5, 4000], np.int32), (1, 1, 1)),
+        "overflow_run": (np.array([1, 0, 70, 4000], np.int32), (1, 1, 1)),
+        "too_few": (np.array([1, 4000, 2, 4000], np.int32), (1, 1, 3)),
+        "extra_ignored": (np.concatenate([good, [5, 6, 0]]).astype(np.int32), sp.shape[:3]),
+        "negative_run": (np.array([0, -3, 5, 4000, 4000], np.int32), (1, 2, 1)),
+        "early_eob_value": (np.array([7, 4000, 9, 4000], np.int32), (1, 1, 2)),
+        "empty": (np.zeros(0, np.int32), (1, 1, 1)),
+        "zero_blocks": (np.zeros(0, np.int32), (0, 1, 1)),
+    }
+    for k, (sym, shape) in cases.items():
+        z[f"err_{k}_sym"] = sym
+        z[f"err_{k}_shape"] = np.array(shape)
+        try:
+            z[f"err_{k}_out"] = _quiet(Z.decode, sym, shape)
+            z[f"err_{k}_exc"] = np.array("")
+        except Exception as e:  # noqa: BLE001  (the reference's exception is the fixture)
+            z[f"err_{k}_exc"] = np.array(f"{type(e).__name__}: {e}")
+    np.savez_compressed(os.path.join(OUT, "zerorun.npz"), **z)
 
 
 if __name__ == "__main__":

@@ -116,3 +116,37 @@ def test_c_oracle_mc_golden(golden):
     m = golden("motion")
     assert bits_equal(c_motion_compensate(m["mc_ref1"], m["mc_mv"], 4), m["mc_out1"])
     assert bits_equal(c_motion_compensate(m["mc_ref3"], m["mc_mv"], 4), m["mc_out3"])
+
+
+ZR_ENC = ["zz1", "zz3", "sparse", "eob1000", "bs16"]
+ZR_ERR = ["truncated", "trailing_zero", "truncated_mid", "ends_after_zero", "ends_after_zero2",
+          "overflow", "overflow_run", "too_few", "extra_ignored", "negative_run",
+          "early_eob_value", "empty"]
+
+
+@pytest.mark.parametrize("case", ZR_ENC)
+def test_zerorun_encode_golden(golden, case):
+    z = golden("zerorun")
+    x, eob, bs = z[f"{case}_x"], int(z[f"{case}_eob"]), int(z[f"{case}_bs"])
+    assert bits_equal(O.zerorun_encode(x, eob, bs), z[f"{case}_sym"])
+    assert bits_equal(O.zerorun_encode_fast(x, eob, bs), z[f"{case}_sym"])
+
+
+def test_zerorun_decode_golden(golden):
+    z = golden("zerorun")
+    assert bits_equal(O.zerorun_decode(z["sparse_sym"], z["sparse_x"].shape[:3]), z["dec_sparse"])
+    assert bits_equal(O.zerorun_decode(z["zz3_sym"], z["zz3_x"].shape[:3]), z["dec_zz3"])
+
+
+@pytest.mark.parametrize("case", ZR_ERR)
+def test_zerorun_decode_errors_golden(golden, case):
+    """The decoder's outcome on malformed / edge streams, exception type and message
+    included, as the reference produced it."""
+    z = golden("zerorun")
+    sym, shape, exc = z[f"err_{case}_sym"], tuple(int(v) for v in z[f"err_{case}_shape"]), str(z[f"err_{case}_exc"])
+    if exc:
+        with pytest.raises(Exception) as ei:
+            O.zerorun_decode(sym, shape)
+        assert f"{type(ei.value).__name__}: {ei.value}" == exc
+    else:
+        assert bits_equal(O.zerorun_decode(sym, shape), z[f"err_{case}_out"])
