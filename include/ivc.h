@@ -168,6 +168,32 @@ int ivc_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, 
 int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
                           int64_t* hist, void* stream);
 
+/* ---------------------------------------------------------------- zero-run coding -- */
+/* ZeroRunCoder.encode (ivclab/entropy/zerorun.py:10-43): src holds nblk rows of row_stride
+ * int32 coefficients in (h w c) order; the first block_size (0..64, <= row_stride) of each
+ * row are coded: nonzero values as themselves, each zero run before the row's last nonzero
+ * as (0, run length), then eob.  The int32 stream goes to out (at most capacity symbols are
+ * written); *nsym = its full length.  Returns IVC_E_SHAPE (with *nsym set) when the stream
+ * is longer than capacity (bound: nblk * (block_size + (block_size + 1) / 2 + 1)).       */
+int ivc_zerorun_encode(const int32_t* src, int64_t nblk, int32_t row_stride, int32_t block_size,
+                       int32_t eob, int32_t* out, int64_t capacity, int64_t* nsym);
+/* Device variant: offsets (device, nblk + 1 int64) receives each block's first symbol and
+ * offsets[nblk] = the stream length; symbols past capacity are not written.  Asynchronous. */
+int ivc_zerorun_encode_dev(const int32_t* src, int64_t nblk, int32_t row_stride,
+                           int32_t block_size, int32_t eob, int64_t* offsets, int32_t* out,
+                           int64_t capacity, void* stream);
+/* ZeroRunCoder.decode (zerorun.py:46-88) of nsym (< 2^32) symbols into nblk blocks of
+ * block_size int32 (out, zero-filled first).  The stream's own errors are results, not
+ * failures: err[0] = 0 decoded; 1 "Block size exceeded: err[1]" (first in stream order);
+ * 2 "Unexpected end of encoded symbols"; 3 the stream ends right after a zero symbol (the
+ * reference's IndexError reading the run length at index err[1]); 4 "Expected err[1]
+ * blocks, got err[2]".  Symbols after the nblk-th block are ignored, as in the reference. */
+int ivc_zerorun_decode(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
+                       int32_t eob, int32_t* out, int64_t* err);
+/* Device variant: every pointer is device memory (err: 3 int64).  Asynchronous.           */
+int ivc_zerorun_decode_dev(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
+                           int32_t eob, int32_t* out, int64_t* err, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,7 @@ reference's NumPy/SciPy results bit for bit; there is no CPU fallback.
     from ivclab_amd.utils import ZigZag, Patcher
     from ivclab_amd.signal.zigzag import zigzag_scan
     from ivclab_amd.video import MotionCompensator
+    from ivclab_amd.entropy import ZeroRunCoder
 
 `install_as_ivclab()` registers these modules under the reference's import paths
 (ivclab.signal, ivclab.signal.dct, ...) so unchanged callers pick them up.
@@ -22,6 +23,7 @@ import types
 from .quantization import PatchQuant  # noqa: F401
 from .signal import DiscreteCosineTransform  # noqa: F401
 from .utils import Patcher, ZigZag  # noqa: F401
+from .entropy import ZeroRunCoder  # noqa: F401
 from .video import MotionCompensator  # noqa: F401
 
 __version__ = "0.1.0"
@@ -37,6 +39,8 @@ _ALIASES = {
     "ivclab.utils.metrics": "ivclab_amd.utils.metrics",
     "ivclab.video": "ivclab_amd.video",
     "ivclab.video.motion": "ivclab_amd.video.motion",
+    "ivclab.entropy": "ivclab_amd.entropy",
+    "ivclab.entropy.zerorun": "ivclab_amd.entropy.zerorun",
 }
 
 
@@ -52,5 +56,6 @@ def install_as_ivclab() -> None:
         sys.modules[name] = mod
         parent, _, leaf = name.rpartition(".")
         setattr(sys.modules[parent], leaf, mod)
-    for cls in (PatchQuant, DiscreteCosineTransform, Patcher, ZigZag, MotionCompensator):
+    for cls in (PatchQuant, DiscreteCosineTransform, Patcher, ZigZag, MotionCompensator,
+                ZeroRunCoder):
         setattr(root, cls.__name__, cls)

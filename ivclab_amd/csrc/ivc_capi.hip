@@ -489,6 +489,104 @@ int ivc_histogram_i32(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, 
   return st.sync();
 }
 
+// ---------------------------------------------------------------- zero-run coding -----
+static int check_zr(int64_t nblk, int32_t stride, int32_t B) {
+  CHECK(nblk >= 0, IVC_E_ARG, "zerorun: nblk must be >= 0");
+  CHECK(B >= 0 && B <= 64, IVC_E_SHAPE, "zerorun: block_size must be in [0, 64]");
+  CHECK(stride >= B && stride >= 1, IVC_E_SHAPE, "zerorun: row_stride must be >= block_size");
+  return IVC_OK;
+}
+
+int ivc_zerorun_encode_dev(const int32_t* src, int64_t nblk, int32_t row_stride,
+                           int32_t block_size, int32_t eob, int64_t* offsets, int32_t* out,
+                           int64_t capacity, void* stream) {
+  TRY(check_zr(nblk, row_stride, block_size));
+  CHECK(capacity >= 0, IVC_E_ARG, "zerorun: capacity must be >= 0");
+  hipStream_t s = (hipStream_t)stream;
+  int32_t* counts = nullptr;
+  int64_t* agg = nullptr;
+  if (nblk > 0) {
+    hipError_t e = hipMallocAsync((void**)&counts, (size_t)nblk * 4, s);
+    if (e == hipSuccess) e = hipMallocAsync((void**)&agg, (size_t)scan_scratch_elems(nblk) * 8, s);
+    if (e != hipSuccess) return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  }
+  int rc = dev_launch(launch_zerorun_offsets(src, nblk, row_stride, block_size, counts, agg, offsets, s),
+                      "zerorun_encode");
+  if (!rc)
+    rc = dev_launch(launch_zerorun_emit(src, nblk, row_stride, block_size, eob, offsets, out, capacity, s),
+                    "zerorun_encode");
+  if (counts) (void)hipFreeAsync(counts, s);
+  if (agg) (void)hipFreeAsync(agg, s);
+  return rc;
+}
+
+int ivc_zerorun_encode(const int32_t* src, int64_t nblk, int32_t row_stride, int32_t block_size,
+                       int32_t eob, int32_t* out, int64_t capacity, int64_t* nsym) {
+  TRY(check_zr(nblk, row_stride, block_size));
+  CHECK(nsym, IVC_E_ARG, "zerorun: nsym is NULL");
+  CHECK(capacity >= 0, IVC_E_ARG, "zerorun: capacity must be >= 0");
+  Staging st;
+  TRY(st.open());
+  const int32_t* d_src = (const int32_t*)st.in(src, (size_t)nblk * row_stride * 4);
+  int32_t* counts = (int32_t*)st.alloc((size_t)nblk * 4);
+  int64_t* agg = (int64_t*)st.alloc((size_t)scan_scratch_elems(nblk) * 8);
+  int64_t* off = (int64_t*)st.alloc((size_t)(nblk + 1) * 8);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_zerorun_offsets(d_src, nblk, row_stride, block_size, counts, agg, off,
+                                         st.ctx->stream), "zerorun_encode"));
+  int64_t total = 0;
+  TRY(st.out(&total, off + nblk, 8));
+  TRY(st.sync());
+  *nsym = total;
+  if (total > capacity)
+    return fail(IVC_E_SHAPE, "zerorun_encode: the stream holds " + std::to_string(total) +
+                                 " symbols, more than capacity " + std::to_string(capacity));
+  int32_t* d_out = (int32_t*)st.alloc((size_t)total * 4);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_zerorun_emit(d_src, nblk, row_stride, block_size, eob, off, d_out, total,
+                                      st.ctx->stream), "zerorun_encode"));
+  TRY(st.out(out, d_out, (size_t)total * 4));
+  return st.sync();
+}
+
+static int check_zr_dec(int64_t nsym, int64_t nblk, int32_t B) {
+  CHECK(nsym >= 0 && nsym < (1LL << 32), IVC_E_ARG, "zerorun_decode: need 0 <= nsym < 2^32");
+  CHECK(nblk >= 0, IVC_E_ARG, "zerorun_decode: nblk must be >= 0");
+  CHECK(B >= 0 && B <= 64, IVC_E_SHAPE, "zerorun_decode: block_size must be in [0, 64]");
+  return IVC_OK;
+}
+
+int ivc_zerorun_decode_dev(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
+                           int32_t eob, int32_t* out, int64_t* err, void* stream) {
+  TRY(check_zr_dec(nsym, nblk, block_size));
+  hipStream_t s = (hipStream_t)stream;
+  void* scratch = nullptr;
+  hipError_t e = hipMallocAsync(&scratch, (size_t)zr_decode_scratch_bytes(nsym), s);
+  if (e != hipSuccess) return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  const int rc = dev_launch(launch_zerorun_decode(sym, nsym, nblk, block_size, eob, out, scratch, err, s),
+                            "zerorun_decode");
+  (void)hipFreeAsync(scratch, s);
+  return rc;
+}
+
+int ivc_zerorun_decode(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
+                       int32_t eob, int32_t* out, int64_t* err) {
+  TRY(check_zr_dec(nsym, nblk, block_size));
+  CHECK(err, IVC_E_ARG, "zerorun_decode: err is NULL");
+  Staging st;
+  TRY(st.open());
+  const int32_t* d_sym = (const int32_t*)st.in(sym, (size_t)nsym * 4);
+  void* scratch = st.alloc((size_t)zr_decode_scratch_bytes(nsym));
+  int32_t* d_out = (int32_t*)st.alloc((size_t)nblk * block_size * 4);
+  int64_t* d_err = (int64_t*)st.alloc(3 * 8);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_zerorun_decode(d_sym, nsym, nblk, block_size, eob, d_out, scratch, d_err,
+                                        st.ctx->stream), "zerorun_decode"));
+  TRY(st.out(out, d_out, (size_t)nblk * block_size * 4));
+  TRY(st.out(err, d_err, 3 * 8));
+  return st.sync();
+}
+
 int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist,
                           void* stream) {
   CHECK(n >= 0 && nbins > 0, IVC_E_ARG, "histogram: need n >= 0 and nbins > 0");

@@ -1,0 +1,414 @@
+// ivc_entropy.hip — zero-run coding of zig-zag blocks on gfx950 (ZeroRunCoder,
+// ivclab/entropy/zerorun.py:10-88): the consumer of the fused encoder's zig-zag output and
+// the producer of the Huffman alphabet.
+//
+// Encode (one wave per block, lane i = coefficient i): the block's nonzero mask is one
+// wave ballot; the last nonzero index, the zero-run starts and the symbol count are scalar
+// bit operations on that mask, and each lane finds its output slot with mbcnt (popcount of
+// the mask bits below it).  Three passes: per-block symbol counts -> exclusive int64 scan
+// -> emission at the block offsets.
+//
+// Decode: a symbol is a run-length slot iff it follows an odd number of consecutive zero
+// symbols (the parse alternates value / run-length slots inside a run of zeros, and any
+// nonzero symbol is followed by a value slot).  One max-scan types every slot; one scan of
+// (EOB count, segmented intra-block length) places every value; the first block overflow
+// in stream order and the end-of-stream cases reproduce the reference's errors.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ivc_internal.h"
+
+namespace ivc {
+
+// ---------------------------------------------------------------- generic tile scan ---
+// Exclusive scan of gen(i), i in [0, n), with an associative Op over T; sink(i, excl, v)
+// receives every element's exclusive prefix.  Three kernels: tile aggregates, a one-
+// workgroup scan of the aggregates, and the tile-local scan.  Each thread owns SCAN_I
+// consecutive elements.
+constexpr int SCAN_T = 256, SCAN_I = 8, SCAN_TILE = SCAN_T * SCAN_I;
+
+// (EOB value slots before, segment-contains-EOB flag, length since the last EOB): the
+// decoder's scan state (declared here so the shuffle overloads precede the templates)
+struct ZrState {
+  int64_t blocks;
+  int64_t reset;
+  int64_t len;
+};
+
+__device__ __forceinline__ int64_t shfl_up_t(int64_t v, int d) {
+  return (int64_t)__shfl_up((long long)v, (unsigned)d);
+}
+__device__ __forceinline__ ZrState shfl_up_t(const ZrState& v, int d) {
+  return ZrState{shfl_up_t(v.blocks, d), shfl_up_t(v.reset, d), shfl_up_t(v.len, d)};
+}
+
+template <typename T, typename Op>
+__device__ T wave_incl_scan(T v, Op op) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const T o = shfl_up_t(v, d);
+    if (lane >= d) v = op(o, v);
+  }
+  return v;
+}
+
+// exclusive scan of one value per thread over the 256-thread workgroup; returns the
+// exclusive prefix, total = workgroup aggregate
+template <typename T, typename Op>
+__device__ T wg_excl_scan(T v, Op op, T* lds4, T& total) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const T incl = wave_incl_scan(v, op);
+  if (lane == 63) lds4[wave] = incl;
+  __syncthreads();
+  T before = Op::identity();
+  for (int w = 0; w < wave; ++w) before = op(before, lds4[w]);
+  total = op(op(op(lds4[0], lds4[1]), lds4[2]), lds4[3]);
+  __syncthreads();
+  const T excl_in_wave = shfl_up_t(incl, 1);
+  return op(before, lane == 0 ? Op::identity() : excl_in_wave);
+}
+
+template <typename T, typename Op, typename Gen>
+__global__ __launch_bounds__(SCAN_T) void scan_tile_aggregate(int64_t n, Gen gen, Op op, T* agg) {
+  __shared__ T lds4[4];
+  const int64_t i0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+  T v = Op::identity();
+#pragma unroll
+  for (int k = 0; k < SCAN_I; ++k)
+    if (i0 + k < n) v = op(v, gen(i0 + k));
+  T total;
+  (void)wg_excl_scan(v, op, lds4, total);
+  if (threadIdx.x == 0) agg[blockIdx.x] = total;
+}
+
+// exclusive scan of the tile aggregates in place (one workgroup); agg[ntiles] = total
+template <typename T, typename Op>
+__global__ __launch_bounds__(SCAN_T) void scan_aggregates(T* agg, int64_t ntiles, Op op) {
+  __shared__ T lds4[4];
+  T carry = Op::identity();
+  for (int64_t base = 0; base < ntiles; base += SCAN_T) {
+    const int64_t i = base + threadIdx.x;
+    const T v = i < ntiles ? agg[i] : Op::identity();
+    T total;
+    const T ex = wg_excl_scan(v, op, lds4, total);
+    if (i < ntiles) agg[i] = op(carry, ex);
+    carry = op(carry, total);
+  }
+  if (threadIdx.x == 0) agg[ntiles] = carry;
+}
+
+template <typename T, typename Op, typename Gen, typename Sink>
+__global__ __launch_bounds__(SCAN_T) void scan_tile_apply(int64_t n, Gen gen, Op op,
+                                                          const T* agg, Sink sink) {
+  __shared__ T lds4[4];
+  const int64_t i0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+  T vals[SCAN_I];
+  T v = Op::identity();
+#pragma unroll
+  for (int k = 0; k < SCAN_I; ++k) {
+    vals[k] = i0 + k < n ? gen(i0 + k) : Op::identity();
+    v = op(v, vals[k]);
+  }
+  T total;
+  T run = op(agg[blockIdx.x], wg_excl_scan(v, op, lds4, total));
+#pragma unroll
+  for (int k = 0; k < SCAN_I; ++k) {
+    if (i0 + k < n) sink(i0 + k, run, vals[k]);
+    run = op(run, vals[k]);
+  }
+}
+
+// agg: device scratch of >= ntiles + 1 elements
+template <typename T, typename Op, typename Gen, typename Sink>
+static hipError_t device_scan(int64_t n, Gen gen, Op op, Sink sink, T* agg, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  scan_tile_aggregate<T, Op, Gen><<<(unsigned)ntiles, SCAN_T, 0, s>>>(n, gen, op, agg);
+  scan_aggregates<T, Op><<<1, SCAN_T, 0, s>>>(agg, ntiles, op);
+  scan_tile_apply<T, Op, Gen, Sink><<<(unsigned)ntiles, SCAN_T, 0, s>>>(n, gen, op, agg, sink);
+  return hipGetLastError();
+}
+
+int64_t scan_scratch_elems(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
+
+struct SumI64 {
+  __device__ int64_t operator()(int64_t a, int64_t b) const { return a + b; }
+  __device__ static int64_t identity() { return 0; }
+};
+struct MaxI64 {
+  __device__ int64_t operator()(int64_t a, int64_t b) const { return a > b ? a : b; }
+  __device__ static int64_t identity() { return INT64_MIN; }
+};
+
+// ---------------------------------------------------------------- encode --------------
+// Per-block symbol stream of zerorun.py:18-38 from the 64-bit nonzero mask m of the first
+// B coefficients: last = highest set bit; inside = bits [0, last]; run starts = zeros
+// inside whose predecessor is nonzero (or i = 0); count = |m| + 2 |starts| + 1 (EOB).
+struct ZrMask {
+  uint64_t m, starts;
+  int last;
+};
+
+__device__ __forceinline__ ZrMask zr_mask(int32_t x, bool valid) {
+  ZrMask z;
+  z.m = __ballot(valid && x != 0);
+  z.last = z.m ? 63 - __builtin_clzll(z.m) : -1;
+  const uint64_t inside = z.last < 0 ? 0ull : (z.last == 63 ? ~0ull : ((1ull << (z.last + 1)) - 1));
+  const uint64_t zeros = ~z.m & inside;
+  z.starts = zeros & ~(zeros << 1);
+  return z;
+}
+
+__device__ __forceinline__ uint32_t popc_below(uint64_t mask) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                   __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// blocks handled per wave-iteration (independent loads in flight)
+constexpr int ZR_UNROLL = 4;
+
+__global__ __launch_bounds__(256) void zr_count_kernel(const int32_t* __restrict__ src,
+                                                       int64_t nblk, int stride, int B,
+                                                       int32_t* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const bool valid = lane < B;
+  for (int64_t b0 = wave * ZR_UNROLL; b0 < nblk; b0 += nw * ZR_UNROLL) {
+    int32_t x[ZR_UNROLL];
+#pragma unroll
+    for (int u = 0; u < ZR_UNROLL; ++u)
+      x[u] = (valid && b0 + u < nblk) ? __builtin_nontemporal_load(src + (b0 + u) * stride + lane) : 0;
+#pragma unroll
+    for (int u = 0; u < ZR_UNROLL; ++u) {
+      const ZrMask z = zr_mask(x[u], valid);
+      if (lane == 0 && b0 + u < nblk)
+        counts[b0 + u] = __builtin_popcountll(z.m) + 2 * __builtin_popcountll(z.starts) + 1;
+    }
+  }
+}
+
+struct CountGen {
+  const int32_t* c;
+  __device__ int64_t operator()(int64_t i) const { return c[i]; }
+};
+struct OffsetSink {
+  int64_t* off;
+  int64_t n;
+  __device__ void operator()(int64_t i, int64_t excl, int64_t v) const {
+    off[i] = excl;
+    if (i == n - 1) off[n] = excl + v;
+  }
+};
+
+__global__ __launch_bounds__(256) void zr_emit_kernel(const int32_t* __restrict__ src, int64_t nblk,
+                                                      int stride, int B, int32_t eob,
+                                                      const int64_t* __restrict__ off,
+                                                      int32_t* __restrict__ out, int64_t capacity) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const bool valid = lane < B;
+  for (int64_t b0 = wave * ZR_UNROLL; b0 < nblk; b0 += nw * ZR_UNROLL) {
+    int32_t x[ZR_UNROLL];
+#pragma unroll
+    for (int u = 0; u < ZR_UNROLL; ++u)
+      x[u] = (valid && b0 + u < nblk) ? __builtin_nontemporal_load(src + (b0 + u) * stride + lane) : 0;
+#pragma unroll
+    for (int u = 0; u < ZR_UNROLL; ++u) {
+      const int64_t blk = b0 + u;
+      if (blk >= nblk) break;
+      const ZrMask z = zr_mask(x[u], valid);
+      const int64_t base = off[blk];
+      const int64_t cnt = __builtin_popcountll(z.m) + 2 * __builtin_popcountll(z.starts) + 1;
+      // the stream is written only while it fits the caller's capacity
+      const int64_t lim = capacity - base;
+      const bool nz = (z.m >> lane) & 1ull, st = (z.starts >> lane) & 1ull;
+      const int64_t p = (int64_t)popc_below(z.m) + 2 * (int64_t)popc_below(z.starts);
+      if (nz && p < lim) out[base + p] = x[u];
+      if (st) {
+        // run length = distance to the next nonzero coefficient (one exists: the run ends
+        // before `last`)
+        const int run = __builtin_ctzll(z.m >> lane);
+        if (p < lim) out[base + p] = 0;
+        if (p + 1 < lim) out[base + p + 1] = run;
+      }
+      if (lane == 0 && cnt - 1 < lim) out[base + cnt - 1] = eob;
+    }
+  }
+}
+
+static unsigned zr_grid(int64_t nblk) {
+  const int64_t waves = (nblk + ZR_UNROLL - 1) / ZR_UNROLL;
+  int64_t grid = (waves + 3) / 4;
+  if (grid > 256 * 16) grid = 256 * 16;
+  return (unsigned)(grid < 1 ? 1 : grid);
+}
+
+// off[0..nblk]: exclusive symbol offsets of the blocks, off[nblk] = stream length.
+// Scratch: counts int32[nblk], agg int64[scan_scratch_elems(nblk)].
+hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, int B,
+                                  int32_t* counts, int64_t* agg, int64_t* off, hipStream_t s) {
+  if (nblk <= 0) return hipMemsetAsync(off, 0, sizeof(int64_t), s);
+  zr_count_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, counts);
+  return device_scan<int64_t>(nblk, CountGen{counts}, SumI64{}, OffsetSink{off, nblk}, agg, s);
+}
+
+// symbols of every block at its offset; symbols at or past `capacity` are not written
+hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
+                               const int64_t* off, int32_t* out, int64_t capacity, hipStream_t s) {
+  if (nblk <= 0) return hipSuccess;
+  zr_emit_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, eob, off, out, capacity);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------- decode --------------
+// Slot typing: lastnz(i) = index of the last nonzero symbol before i (max-scan); slot i is
+// a run-length slot iff i - 1 - lastnz(i) is odd.
+struct NzPosGen {
+  const int32_t* s;
+  __device__ int64_t operator()(int64_t i) const { return s[i] != 0 ? i : -1; }
+};
+struct RlTypeSink {
+  uint8_t* is_rl;
+  __device__ void operator()(int64_t i, int64_t excl, int64_t) const {
+    const int64_t last = excl < -1 ? -1 : excl;     // identity (no nonzero before) -> -1
+    is_rl[i] = (uint8_t)(((i - 1 - last) & 1) != 0);
+  }
+};
+
+// segmented scan: the EOB value slot resets the length and contributes 0 to it
+struct ZrOp {
+  __device__ ZrState operator()(const ZrState& a, const ZrState& b) const {
+    ZrState r;
+    r.blocks = a.blocks + b.blocks;
+    r.reset = a.reset | b.reset;
+    r.len = b.reset ? b.len : a.len + b.len;
+    return r;
+  }
+  __device__ static ZrState identity() { return ZrState{0, 0, 0}; }
+};
+
+__device__ __forceinline__ int64_t zr_run_of(const int32_t* s, int64_t i, int64_t n) {
+  if (i + 1 >= n) return 0;
+  const int64_t r = s[i + 1];
+  return r < 0 ? 0 : r;      // [0] * negative = []
+}
+
+struct ZrGen {
+  const int32_t* s;
+  const uint8_t* is_rl;
+  int64_t n;
+  int32_t eob;
+  __device__ ZrState operator()(int64_t i) const {
+    if (is_rl[i]) return ZrState{0, 0, 0};
+    const int32_t v = s[i];
+    if (v == eob) return ZrState{1, 1, 0};
+    return ZrState{0, 0, v == 0 ? zr_run_of(s, i, n) : 1};
+  }
+};
+
+struct ZrSink {
+  const int32_t* s;
+  const uint8_t* is_rl;
+  int64_t n, expected;
+  int B;
+  int32_t eob;
+  int32_t* out;
+  unsigned long long* first_overflow;   // (slot << 32) | length, minimum over overflows
+  __device__ void operator()(int64_t i, const ZrState& ex, const ZrState& v) const {
+    if (is_rl[i] || ex.blocks >= expected) return;
+    const int32_t sym = s[i];
+    if (sym == eob) return;
+    const int64_t pos = ex.len;                       // length of the block before slot i
+    const int64_t after = pos + v.len;                // len(block) after this slot
+    if (sym != 0 && pos < B) out[ex.blocks * B + pos] = sym;
+    if (sym == 0 && i + 1 >= n) return;               // ends after a zero: handled at the end
+    if (after > B) {
+      const uint64_t L = after > 0xffffffffll ? 0xffffffffull : (uint64_t)after;
+      atomicMin(first_overflow, ((unsigned long long)i << 32) | L);
+    }
+  }
+};
+
+// err[0] = code (0 ok, 1 block size exceeded, 2 unexpected end, 3 ended right after a zero
+// symbol, 4 too few blocks), err[1], err[2] = message arguments
+__global__ void zr_decode_verdict(const int32_t* s, const uint8_t* is_rl, int64_t n,
+                                  int64_t expected, int32_t eob, const ZrState* total,
+                                  const unsigned long long* first_overflow, int64_t* err) {
+  const unsigned long long ov = *first_overflow;
+  int64_t code = 0, a0 = 0, a1 = 0;
+  const int64_t got = n > 0 ? total->blocks : 0;
+  if (ov != ~0ull) {
+    code = 1;
+    a0 = (int64_t)(ov & 0xffffffffull);
+  } else if (got < expected) {
+    const bool last_value = n > 0 && !is_rl[n - 1];
+    if (n > 0 && last_value && s[n - 1] == 0) {
+      code = 3;
+      a0 = n;
+    } else if (n == 0 || (last_value && s[n - 1] == eob)) {
+      code = 4;
+      a0 = expected;
+      a1 = got;
+    } else {
+      code = 2;
+    }
+  }
+  err[0] = code;
+  err[1] = a0;
+  err[2] = a1;
+}
+
+struct ZrTotalSink {
+  ZrState* total;
+  int64_t n;
+  __device__ void operator()(int64_t i, const ZrState& ex, const ZrState& v) const {
+    if (i == n - 1) *total = ZrOp{}(ex, v);
+  }
+};
+
+template <typename A, typename B2>
+struct BothSinks {
+  A a;
+  B2 b;
+  __device__ void operator()(int64_t i, const ZrState& ex, const ZrState& v) const {
+    a(i, ex, v);
+    b(i, ex, v);
+  }
+};
+
+int64_t zr_decode_scratch_bytes(int64_t n) {
+  // is_rl (n bytes, 16-aligned) + int64 aggregates + ZrState aggregates + total + overflow
+  const int64_t nt = scan_scratch_elems(n);
+  return ((n + 15) / 16) * 16 + nt * 8 + nt * (int64_t)sizeof(ZrState) + 64;
+}
+
+hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected, int B,
+                                 int32_t eob, int32_t* out, void* scratch, int64_t* err,
+                                 hipStream_t s) {
+  const int64_t nt = scan_scratch_elems(n);
+  uint8_t* base = (uint8_t*)scratch;
+  uint8_t* is_rl = base;
+  int64_t* agg = (int64_t*)(base + ((n + 15) / 16) * 16);
+  ZrState* zagg = (ZrState*)(agg + nt);
+  ZrState* total = zagg + nt;
+  unsigned long long* ovf = (unsigned long long*)(total + 1);
+  hipError_t e;
+  if ((e = hipMemsetAsync(out, 0, (size_t)expected * B * sizeof(int32_t), s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(ovf, 0xff, sizeof(unsigned long long), s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(total, 0, sizeof(ZrState), s)) != hipSuccess) return e;
+  if (n > 0) {
+    e = device_scan<int64_t>(n, NzPosGen{sym}, MaxI64{}, RlTypeSink{is_rl}, agg, s);
+    if (e != hipSuccess) return e;
+    ZrSink place{sym, is_rl, n, expected, B, eob, out, ovf};
+    e = device_scan<ZrState>(n, ZrGen{sym, is_rl, n, eob}, ZrOp{},
+                             BothSinks<ZrSink, ZrTotalSink>{place, ZrTotalSink{total, n}}, zagg, s);
+    if (e != hipSuccess) return e;
+  }
+  zr_decode_verdict<<<1, 1, 0, s>>>(sym, is_rl, n, expected, eob, total, ovf, err);
+  return hipGetLastError();
+}
+
+}  // namespace ivc

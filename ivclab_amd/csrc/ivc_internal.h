@@ -39,6 +39,16 @@ hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int6
 hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, int unzigzag,
                                double* out, hipStream_t s);
 unsigned resident_grid_ptr(const void* kernel, int64_t work_groups_needed);
+// zero-run coding (ivc_entropy.hip)
+int64_t scan_scratch_elems(int64_t n);
+hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, int B,
+                                  int32_t* counts, int64_t* agg, int64_t* off, hipStream_t s);
+hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
+                               const int64_t* off, int32_t* out, int64_t capacity, hipStream_t s);
+int64_t zr_decode_scratch_bytes(int64_t n);
+hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected, int B,
+                                 int32_t eob, int32_t* out, void* scratch, int64_t* err,
+                                 hipStream_t s);
 hipError_t launch_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
                                 int64_t* hist, hipStream_t s);
 hipError_t launch_histogram(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins,

@@ -94,3 +94,34 @@ def histogram(sym, lo, hist, stream=None):
         raise ValueError(f"histogram: symbols must be int32 or int64, got {sym.dtype}")
     N.check(fn(sym.data_ptr(), sym.numel(), int(lo), hist.numel(), hist.data_ptr(),
                _stream(stream)), "histogram")
+
+
+def zerorun_encode(blocks, offsets, out, block_size=64, eob=4000, stream=None):
+    """blocks [..., p] int32 (zig-zag rows, (h w c) order) -> offsets [nblk + 1] int64
+    (offsets[nblk] = stream length) and the symbols in out (int32, written up to its
+    length).  Asynchronous: read offsets[-1] after the stream to size or check out."""
+    import torch
+    _contig(blocks, "blocks"); _contig(offsets, "offsets"); _contig(out, "out")
+    if blocks.dtype != torch.int32 or offsets.dtype != torch.int64 or out.dtype != torch.int32:
+        raise ValueError("zerorun_encode: blocks/out must be int32 and offsets int64")
+    p = blocks.shape[-1]
+    nblk = blocks.numel() // p if p else 0
+    if offsets.numel() < nblk + 1:
+        raise ValueError("zerorun_encode: offsets needs nblk + 1 entries")
+    N.check(N.lib().ivc_zerorun_encode_dev(blocks.data_ptr(), nblk, p, int(block_size), int(eob),
+                                           offsets.data_ptr(), out.data_ptr(), out.numel(),
+                                           _stream(stream)), "zerorun_encode")
+
+
+def zerorun_decode(sym, nblk, out, err, block_size=64, eob=4000, stream=None):
+    """sym [n] int32 -> out [nblk, block_size] int32; err [3] int64 receives the stream's
+    verdict (0 = decoded; see include/ivc.h).  Asynchronous."""
+    import torch
+    _contig(sym, "sym"); _contig(out, "out"); _contig(err, "err")
+    if sym.dtype != torch.int32 or out.dtype != torch.int32 or err.dtype != torch.int64:
+        raise ValueError("zerorun_decode: sym/out must be int32 and err int64")
+    if out.numel() < nblk * block_size or err.numel() < 3:
+        raise ValueError("zerorun_decode: out needs nblk * block_size entries, err 3")
+    N.check(N.lib().ivc_zerorun_decode_dev(sym.data_ptr(), sym.numel(), int(nblk), int(block_size),
+                                           int(eob), out.data_ptr(), err.data_ptr(),
+                                           _stream(stream)), "zerorun_decode")

@@ -445,3 +445,110 @@ def test_me_exact_u8_full_hd_vs_c_oracle():
     for rows in ((0, 3), (66, 69), (132, 135)):
         want = c_motion_vectors(ref, cur, 16, exact_u8=True, rows=rows)
         assert_bits(mv[rows[0]:rows[1]], want.astype(np.int64), f"1080p rows {rows}")
+
+
+# ------------------------------------------------------------------- zero-run coding ---
+ZR_ENC = ["zz1", "zz3", "sparse", "eob1000", "bs16"]
+ZR_ERR = ["truncated", "trailing_zero", "truncated_mid", "ends_after_zero", "ends_after_zero2",
+          "overflow", "overflow_run", "too_few", "extra_ignored", "negative_run",
+          "early_eob_value", "empty", "zero_blocks"]
+
+
+@pytest.mark.parametrize("case", ZR_ENC)
+def test_zerorun_encode_golden(golden, case):
+    from ivclab_amd.entropy import ZeroRunCoder
+    z = golden("zerorun")
+    Z = ZeroRunCoder(int(z[f"{case}_eob"]), int(z[f"{case}_bs"]))
+    assert_bits(Z.encode(z[f"{case}_x"]), z[f"{case}_sym"], case)
+
+
+def test_zerorun_decode_golden(golden):
+    from ivclab_amd.entropy import ZeroRunCoder
+    z = golden("zerorun")
+    Z = ZeroRunCoder()
+    assert_bits(Z.decode(z["sparse_sym"], z["sparse_x"].shape[:3]), z["dec_sparse"], "sparse")
+    assert_bits(Z.decode(z["zz3_sym"], z["zz3_x"].shape[:3]), z["dec_zz3"], "zz3")
+
+
+@pytest.mark.parametrize("case", ZR_ERR)
+def test_zerorun_decode_errors_golden(golden, case):
+    from ivclab_amd.entropy import ZeroRunCoder
+    z = golden("zerorun")
+    sym, shape = z[f"err_{case}_sym"], tuple(int(v) for v in z[f"err_{case}_shape"])
+    exc = str(z[f"err_{case}_exc"])
+    if exc:
+        with pytest.raises(Exception) as ei:
+            ZeroRunCoder().decode(sym, shape)
+        assert f"{type(ei.value).__name__}: {ei.value}" == exc
+    else:
+        assert_bits(ZeroRunCoder().decode(sym, shape), z[f"err_{case}_out"], case)
+
+
+@pytest.mark.parametrize("bs,p", [(64, 64), (16, 16), (10, 64), (0, 8), (64, 80)])
+def test_zerorun_random_vs_oracle(bs, p):
+    """Large random sparse streams (mixed densities, all-zero / full / alternating blocks)
+    against the oracle, then the decoder's round trip."""
+    from ivclab_amd.entropy import ZeroRunCoder
+    rng = np.random.default_rng(bs * 100 + p)
+    nblk = 30000
+    x = rng.integers(-200, 201, (nblk, p)).astype(np.int32)
+    dens = rng.random((nblk, 1))
+    x[rng.random((nblk, p)) > dens] = 0
+    x[:50] = 0
+    x[50:100, :] = np.where(np.arange(p) % 2 == 0, 5, 0)
+    x[100:150] = rng.integers(1, 9, (50, p))
+    x4 = x.reshape(10, 30, 100, p)
+    Z = ZeroRunCoder(4000, bs)
+    got = Z.encode(x4)
+    want = O.zerorun_encode_fast(x[:, :bs] if bs else np.zeros((nblk, 0), np.int32), 4000, bs) if bs \
+        else np.full(nblk, 4000, np.int32)
+    assert_bits(got, want, "encode")
+    dec = Z.decode(got, (10, 30, 100))
+    assert_bits(dec.reshape(nblk, bs), x[:, :bs], "round trip")
+
+
+def test_zerorun_device_api_and_capacity():
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(77)
+    x = rng.integers(-9, 10, (5000, 64)).astype(np.int32)
+    x[rng.random(x.shape) < 0.7] = 0
+    want = O.zerorun_encode_fast(x)
+    blocks = torch.from_numpy(x).cuda()
+    off = torch.empty(5001, dtype=torch.int64, device="cuda")
+    out = torch.full((want.size,), -1, dtype=torch.int32, device="cuda")
+    D.zerorun_encode(blocks, off, out)
+    torch.cuda.synchronize()
+    assert int(off[-1]) == want.size
+    assert np.array_equal(out.cpu().numpy(), want)
+    # a short buffer: only the prefix that fits is written, the length is still reported
+    short = torch.full((1000,), -1, dtype=torch.int32, device="cuda")
+    D.zerorun_encode(blocks, off, short)
+    torch.cuda.synchronize()
+    assert int(off[-1]) == want.size
+    assert np.array_equal(short.cpu().numpy(), want[:1000])
+    # device decode
+    dec = torch.empty((5000, 64), dtype=torch.int32, device="cuda")
+    err = torch.empty(3, dtype=torch.int64, device="cuda")
+    D.zerorun_decode(out, 5000, dec, err)
+    torch.cuda.synchronize()
+    assert err.cpu().tolist() == [0, 0, 0]
+    assert np.array_equal(dec.cpu().numpy(), x)
+
+
+def test_zerorun_after_fused_intra():
+    """The codec chain: fused intra encode with zig-zag -> zero-run stream -> decode ->
+    back to the quantised blocks, against the oracle's chain."""
+    from ivclab_amd.entropy import ZeroRunCoder
+    N, L = _native()
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (1, 64, 96, 1), dtype=np.uint8)
+    img[0, :24] = 128
+    t = N.table_arg(PatchQuant(0.5).get_quantization_table())
+    zz = np.empty((8, 12, 3, 64), np.int32)
+    N.check(L.ivc_intra_encode(N.ptr(img), 1, 1, 64, 96, 1, N.ptr(t), N.F64, 1, N.ptr(zz)))
+    want_zz = O.intra_encode(img[0], 0.5, zigzag=True)
+    assert_bits(zz, want_zz, "zig-zag")
+    sym = ZeroRunCoder().encode(zz)
+    assert_bits(sym, O.zerorun_encode(want_zz), "stream")
+    assert_bits(ZeroRunCoder().decode(sym, (8, 12, 3)), want_zz, "decoded")
