@@ -196,7 +196,9 @@ def main():
     dist, rank, world, local = dist_setup(args.gpus)
     dev = torch.device("cuda", torch.cuda.current_device())
     import ivclab_amd.device as D
-    from ivclab_amd.distributed import global_histogram
+    from ivclab_amd.distributed import global_bounds, global_histogram
+    from ivclab_amd.entropy.stats import (entropy_bits, huffman_bounds, smooth_pmf,
+                                          stats_marg_from_counts)
     from ivclab_amd import PatchQuant
     table = PatchQuant(1.0).get_quantization_table()
 
@@ -221,16 +223,33 @@ def main():
     algo_bytes = px_step * 13                        # 1 B u8 in + 3 x 4 B int32 out per px
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
 
-    # exchange for the global Huffman table: per-rank histogram + one all-gather
-    hist = torch.zeros(HIST_BINS, dtype=torch.int64, device=dev)
+    # ---- symbols for the global Huffman table (IntraCodec.image2symbols + training input,
+    # intracodec.py:32-90,149-166): the same frames with zig-zag, zero-run coded on the GPU;
+    # global alphabet bounds (one all-reduce), per-rank histogram, one all-gather
+    D.intra_encode(frames, table, out, zigzag=True)
+    nblk = out.numel() // 64
+    blocks = out.view(nblk, 64)
+    offs = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
+    probe = torch.empty(1, dtype=torch.int32, device=dev)
+    D.zerorun_encode(blocks, offs, probe)
+    nsym = int(offs[-1].item())
+    sym = torch.empty(nsym, dtype=torch.int32, device=dev)
+    zwall, zms = timed(dist, lambda: D.zerorun_encode(blocks, offs, sym), 3, 1)
+    mm = torch.empty(2, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     t_ex = time.perf_counter()
-    D.histogram(out.view(-1), HIST_LO, hist)
+    D.minmax(sym, mm)
+    lo, hi = global_bounds(mm)
+    b0, b1 = huffman_bounds(lo, hi)
+    hist = torch.zeros(b1 - b0 - 1, dtype=torch.int64, device=dev)
+    D.histogram(sym, b0, hist)
     ghist = global_histogram(hist)
     torch.cuda.synchronize()
     exchange_ms = (time.perf_counter() - t_ex) * 1e3
-    total_syms = int(ghist.sum().item())
-
+    counts = ghist.cpu().numpy()
+    total_syms = int(counts.sum())
+    pmf = smooth_pmf(stats_marg_from_counts(counts))
+    del sym, offs, blocks
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_intra_latest.json")
     if os.path.exists(pmc):
@@ -260,8 +279,15 @@ def main():
                      "traffic": traffic, "kernel": "fused_encode_kernel<u8,f64,C=1>",
                      "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": algo_bytes,
                      "write_ceiling_GBs": round(fill_gbs, 1)},
-        "exchange": {"histogram_bins": HIST_BINS, "symbols": total_syms, "ms": round(exchange_ms, 3),
-                     "collective": "all_gather_into_tensor (RCCL)" if dist is not None else "none (1 rank)"},
+        "zerorun": {"blocks_per_gpu": nblk, "symbols_per_gpu": nsym,
+                    "ms": round(zms, 3), "Mblocks_per_s": round(nblk / zms / 1e3, 1),
+                    "note": "ZeroRunCoder.encode of the zig-zag output (count, scan, emit kernels)",
+                    "algorithmic_GBs": round((nblk * 256 + nsym * 4) / (zms * 1e-3) / 1e9, 1)},
+        "exchange": {"alphabet": [b0, b1], "bins": b1 - b0 - 1, "symbols": total_syms,
+                     "entropy_bits_per_symbol": round(entropy_bits(pmf), 4),
+                     "ms": round(exchange_ms, 3),
+                     "collective": "all_reduce + all_gather_into_tensor (RCCL)" if dist is not None
+                     else "none (1 rank)"},
     }
     del out, frames
     torch.cuda.empty_cache()

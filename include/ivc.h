@@ -190,6 +190,10 @@ int ivc_zerorun_encode_dev(const int32_t* src, int64_t nblk, int32_t row_stride,
  * blocks, got err[2]".  Symbols after the nblk-th block are ignored, as in the reference. */
 int ivc_zerorun_decode(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
                        int32_t eob, int32_t* out, int64_t* err);
+/* mm[0] = min, mm[1] = max of n int32 symbols (INT32_MAX, INT32_MIN when n = 0): the
+ * Huffman alphabet bounds of IntraCodec.train_huffman_from_image (intracodec.py:161-163). */
+int ivc_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm);
+int ivc_minmax_i32_dev(const int32_t* sym, int64_t n, int32_t* mm, void* stream);
 /* Device variant: every pointer is device memory (err: 3 int64).  Asynchronous.           */
 int ivc_zerorun_decode_dev(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
                            int32_t eob, int32_t* out, int64_t* err, void* stream);

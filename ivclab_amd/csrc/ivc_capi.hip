@@ -587,6 +587,23 @@ int ivc_zerorun_decode(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t b
   return st.sync();
 }
 
+int ivc_minmax_i32_dev(const int32_t* sym, int64_t n, int32_t* mm, void* stream) {
+  CHECK(n >= 0 && mm, IVC_E_ARG, "minmax: need n >= 0 and an output");
+  return dev_launch(launch_minmax_i32(sym, n, mm, (hipStream_t)stream), "minmax");
+}
+
+int ivc_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm) {
+  CHECK(n >= 0 && mm, IVC_E_ARG, "minmax: need n >= 0 and an output");
+  Staging st;
+  TRY(st.open());
+  const int32_t* d_sym = (const int32_t*)st.in(sym, (size_t)n * 4);
+  int32_t* d_mm = (int32_t*)st.alloc(8);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_minmax_i32(d_sym, n, d_mm, st.ctx->stream), "minmax"));
+  TRY(st.out(mm, d_mm, 8));
+  return st.sync();
+}
+
 int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist,
                           void* stream) {
   CHECK(n >= 0 && nbins > 0, IVC_E_ARG, "histogram: need n >= 0 and nbins > 0");

@@ -411,4 +411,42 @@ hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- symbol range --------
+// min / max of an int32 stream: the Huffman alphabet bounds of IntraCodec
+// (ivclab/image/intracodec.py:161-163 takes min - 20, max + 20 + 1).
+__global__ void minmax_init(int32_t* mm) {
+  mm[0] = INT32_MAX;
+  mm[1] = INT32_MIN;
+}
+
+__global__ __launch_bounds__(256) void minmax_kernel(const int32_t* __restrict__ sym, int64_t n,
+                                                     int32_t* mm) {
+  int32_t lo = INT32_MAX, hi = INT32_MIN;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int32_t v = __builtin_nontemporal_load(sym + i);
+    lo = v < lo ? v : lo;
+    hi = v > hi ? v : hi;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const int32_t ol = __shfl_xor(lo, d), oh = __shfl_xor(hi, d);
+    lo = ol < lo ? ol : lo;
+    hi = oh > hi ? oh : hi;
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicMin(&mm[0], lo);
+    atomicMax(&mm[1], hi);
+  }
+}
+
+hipError_t launch_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm, hipStream_t s) {
+  minmax_init<<<1, 1, 0, s>>>(mm);
+  if (n > 0) {
+    int64_t g = (n + 256 * 64 - 1) / (256 * 64);
+    if (g > 256 * 8) g = 256 * 8;
+    minmax_kernel<<<(unsigned)g, 256, 0, s>>>(sym, n, mm);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace ivc

@@ -125,3 +125,13 @@ def zerorun_decode(sym, nblk, out, err, block_size=64, eob=4000, stream=None):
     N.check(N.lib().ivc_zerorun_decode_dev(sym.data_ptr(), sym.numel(), int(nblk), int(block_size),
                                            int(eob), out.data_ptr(), err.data_ptr(),
                                            _stream(stream)), "zerorun_decode")
+
+
+def minmax(sym, mm, stream=None):
+    """mm[0], mm[1] = min, max of the int32 tensor sym (int32 mm of 2)."""
+    import torch
+    _contig(sym, "sym"); _contig(mm, "mm")
+    if sym.dtype != torch.int32 or mm.dtype != torch.int32 or mm.numel() < 2:
+        raise ValueError("minmax: int32 symbols and an int32 output of 2")
+    N.check(N.lib().ivc_minmax_i32_dev(sym.data_ptr(), sym.numel(), mm.data_ptr(),
+                                       _stream(stream)), "minmax")

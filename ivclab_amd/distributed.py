@@ -30,6 +30,18 @@ def shard_pairs(nframes: int, rank: int, world: int) -> tuple:
     return s, e + 1
 
 
+def global_bounds(local_mm, group=None):
+    """(min, max) over every rank of the int32 pairs local_mm = [min, max] (device tensor,
+    ivc_minmax_i32's output) with one all-reduce (MAX of [-min, max] in int64)."""
+    import torch
+    import torch.distributed as dist
+    v = torch.stack([-local_mm[0].to(torch.int64), local_mm[1].to(torch.int64)])
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+    lo, hi = v.tolist()
+    return -lo, hi
+
+
 def global_histogram(local_hist, group=None):
     """Sum of every rank's histogram (a 1-D int64 tensor on this rank's device) via one
     all-gather; every rank receives the same result."""

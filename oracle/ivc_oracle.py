@@ -334,3 +334,22 @@ def zerorun_decode(encoded, original_shape, eob=4000, block_size=64):
     if len(blocks) != expected:
         raise ValueError(f"Expected {expected} blocks, got {len(blocks)}")
     return np.array(blocks, dtype=np.int32).reshape(h, w, c, block_size)
+
+
+# ---------------------------------------------------------------- symbol statistics -----
+def stats_marg(image, pixel_range):
+    """stats_marg (ivclab/entropy/entropy.py:6-29): np.histogram of the float64-cast,
+    flattened data over the bin edges pixel_range, divided by the number of samples.
+    (The module is not importable here — it imports ivclab.utils, whose package __init__
+    needs the absent constriction wheel — so this restatement is pinned by the same NumPy
+    calls, not by fixtures.)"""
+    flat = np.asarray(image).astype(np.float64).flatten()
+    counts, _ = np.histogram(flat, bins=pixel_range)
+    return counts / flat.size
+
+
+def smooth_pmf(pmf, epsilon=1e-9):
+    """entropy.py:31-35."""
+    pmf = pmf + epsilon
+    pmf /= pmf.sum()
+    return pmf

@@ -139,3 +139,17 @@ def test_single_hip_runtime_with_torch(lib):
     maps = open("/proc/self/maps").read().splitlines()
     hips = {ln.split()[-1] for ln in maps if "libamdhip64" in ln}
     assert len(hips) == 1, hips
+
+
+def test_symbol_pmf_from_counts_matches_stats_marg():
+    """The host finish of the Huffman-table input (counts from the GPU histogram) equals
+    the reference's stats_marg + smooth_pmf on the symbol stream itself, bit for bit."""
+    from oracle import ivc_oracle as O
+    from ivclab_amd.entropy.stats import huffman_bounds, smooth_pmf, stats_marg_from_counts
+    rng = np.random.default_rng(9)
+    sym = np.concatenate([rng.integers(-60, 61, 20000), np.full(3000, 4000), [0] * 5000]).astype(np.int32)
+    b0, b1 = huffman_bounds(sym.min(), sym.max())
+    counts = O.histogram(sym, b0, b1 - b0 - 1)        # what ivc_histogram_i32 returns
+    got = smooth_pmf(stats_marg_from_counts(counts))
+    want = O.smooth_pmf(O.stats_marg(sym, np.arange(b0, b1)))
+    assert got.dtype == want.dtype and got.tobytes() == want.tobytes()

@@ -552,3 +552,20 @@ def test_zerorun_after_fused_intra():
     sym = ZeroRunCoder().encode(zz)
     assert_bits(sym, O.zerorun_encode(want_zz), "stream")
     assert_bits(ZeroRunCoder().decode(sym, (8, 12, 3)), want_zz, "decoded")
+
+
+def test_minmax_host_and_device():
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    N, L = _native()
+    rng = np.random.default_rng(8)
+    for n in (0, 1, 7, 100003):
+        x = rng.integers(-(1 << 31), (1 << 31) - 1, n, dtype=np.int64).astype(np.int32)
+        mm = np.zeros(2, np.int32)
+        N.check(L.ivc_minmax_i32(N.ptr(x), n, N.ptr(mm)))
+        want = [x.min(), x.max()] if n else [np.iinfo(np.int32).max, np.iinfo(np.int32).min]
+        assert mm.tolist() == list(map(int, want))
+        t = torch.from_numpy(x).cuda()
+        dm = torch.zeros(2, dtype=torch.int32, device="cuda")
+        D.minmax(t, dm)
+        assert dm.cpu().tolist() == list(map(int, want))
