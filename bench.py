@@ -37,12 +37,24 @@ def dist_setup(n_gpus):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local)
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        return dist, rank, world, local
+        # rehearsal of the multi-rank path on a 1-GPU box: IVC_BENCH_BACKEND=gloo puts every
+        # rank on cuda:0 (RCCL needs one GPU per rank); the driver's runs use nccl = RCCL
+        backend = os.environ.get("IVC_BENCH_BACKEND", "nccl")
+        dev = local if backend == "nccl" else local % torch.cuda.device_count()
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
+        return dist, rank, world, dev
     torch.cuda.set_device(0)
     return None, 0, 1, 0
+
+
+def coll_name(dist):
+    b = dist.get_backend()
+    return "RCCL" if b == "nccl" else b
 
 
 def barrier(dist):
@@ -53,7 +65,8 @@ def barrier(dist):
 def max_over_ranks(dist, v):
     if dist is None:
         return v
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    t = torch.tensor([v], dtype=torch.float64,
+                     device="cpu" if dist.get_backend() == "gloo" else "cuda")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -286,8 +299,8 @@ def main():
         "exchange": {"alphabet": [b0, b1], "bins": b1 - b0 - 1, "symbols": total_syms,
                      "entropy_bits_per_symbol": round(entropy_bits(pmf), 4),
                      "ms": round(exchange_ms, 3),
-                     "collective": "all_reduce + all_gather_into_tensor (RCCL)" if dist is not None
-                     else "none (1 rank)"},
+                     "collective": f"all_reduce + all_gather_into_tensor ({coll_name(dist)})"
+                     if dist is not None else "none (1 rank)"},
     }
     del out, frames
     torch.cuda.empty_cache()
@@ -358,8 +371,8 @@ def main():
             "config": {"workload": f"cfg5: {F5} frames {W5}x{H5} u8 luma split across {world} "
                                    f"rank(s) (+1 halo frame each), sr={sr5}",
                        "pairs_per_rank_max": int(max_over_ranks(dist, float(pairs5)))},
-            "exchange": {"collective": "all_gather_into_tensor (RCCL)" if dist is not None
-                         else "none (1 rank)",
+            "exchange": {"collective": f"all_gather_into_tensor ({coll_name(dist)})"
+                         if dist is not None else "none (1 rank)",
                          "bins": HIST_BINS + nmv,
                          "symbols": int(g5[:HIST_BINS].sum().item()),
                          "motion_vectors": int(g5[HIST_BINS:].sum().item())},

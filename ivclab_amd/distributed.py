@@ -30,6 +30,12 @@ def shard_pairs(nframes: int, rank: int, world: int) -> tuple:
     return s, e + 1
 
 
+def _host_staged(t, group=None):
+    """gloo (CPU rehearsals, tests) has no device-tensor collectives: stage through host."""
+    import torch.distributed as dist
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
 def global_bounds(local_mm, group=None):
     """(min, max) over every rank of the int32 pairs local_mm = [min, max] (device tensor,
     ivc_minmax_i32's output) with one all-reduce (MAX of [-min, max] in int64)."""
@@ -37,6 +43,8 @@ def global_bounds(local_mm, group=None):
     import torch.distributed as dist
     v = torch.stack([-local_mm[0].to(torch.int64), local_mm[1].to(torch.int64)])
     if dist.is_initialized() and dist.get_world_size(group) > 1:
+        if _host_staged(v, group):
+            v = v.cpu()
         dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
     lo, hi = v.tolist()
     return -lo, hi
@@ -50,6 +58,8 @@ def global_histogram(local_hist, group=None):
     if not dist.is_initialized() or dist.get_world_size(group) == 1:
         return local_hist.clone()
     world = dist.get_world_size(group)
+    if _host_staged(local_hist, group):
+        return global_histogram(local_hist.cpu(), group).to(local_hist.device)
     gathered = torch.empty((world,) + tuple(local_hist.shape), dtype=local_hist.dtype,
                            device=local_hist.device)
     try:
