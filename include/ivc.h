@@ -190,6 +190,19 @@ int ivc_zerorun_encode_dev(const int32_t* src, int64_t nblk, int32_t row_stride,
  * blocks, got err[2]".  Symbols after the nblk-th block are ignored, as in the reference. */
 int ivc_zerorun_decode(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
                        int32_t eob, int32_t* out, int64_t* err);
+/* IntraCodec.image2symbols' hot part fused (ivclab/image/intracodec.py:66-81 with
+ * is_source_rgb=False): u8 frames [nframes][H][W][C] (C = 1 or 3, H and W multiples of 8)
+ * -> patch -> DCT -> quantise -> zig-zag -> zero-run symbols, one int32 stream over
+ * frames, then blocks in (h w c) order — the concatenation of ZeroRunCoder.encode of each
+ * frame.  The coefficients never reach memory.  At most capacity symbols are written;
+ * *nsym = the stream length (device int64 for _dev).  Host call: IVC_E_SHAPE with *nsym
+ * set when capacity is too small.                                                        */
+int ivc_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W, int C,
+                      const double* table, int32_t eob, int32_t* out, int64_t capacity,
+                      int64_t* nsym);
+int ivc_intra_symbols_dev(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
+                          int C, const double* table, int32_t eob, int32_t* out,
+                          int64_t capacity, int64_t* nsym, void* stream);
 /* mm[0] = min, mm[1] = max of n int32 symbols (INT32_MAX, INT32_MIN when n = 0): the
  * Huffman alphabet bounds of IntraCodec.train_huffman_from_image (intracodec.py:161-163). */
 int ivc_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm);

@@ -587,6 +587,50 @@ int ivc_zerorun_decode(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t b
   return st.sync();
 }
 
+int ivc_intra_symbols_dev(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
+                          int C, const double* table, int32_t eob, int32_t* out,
+                          int64_t capacity, int64_t* nsym, void* stream) {
+  TRY(check_frames(nframes, H, W, "intra_symbols"));
+  CHECK(C == 1 || C == 3, IVC_E_SHAPE, "intra_symbols: C must be 1 or 3");
+  CHECK(dtype == IVC_U8, IVC_E_DTYPE, "intra_symbols: uint8 frames only");
+  CHECK(capacity >= 0 && nsym, IVC_E_ARG, "intra_symbols: need capacity >= 0 and nsym");
+  QTab t;
+  TRY(load_table(table, &t));
+  return dev_launch(launch_intra_symbols(img, dtype, nframes, H, W, C, t, eob, out, capacity, nsym,
+                                         (hipStream_t)stream), "intra_symbols");
+}
+
+int ivc_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W, int C,
+                      const double* table, int32_t eob, int32_t* out, int64_t capacity,
+                      int64_t* nsym) {
+  TRY(check_frames(nframes, H, W, "intra_symbols"));
+  CHECK(C == 1 || C == 3, IVC_E_SHAPE, "intra_symbols: C must be 1 or 3");
+  CHECK(dtype == IVC_U8, IVC_E_DTYPE, "intra_symbols: uint8 frames only");
+  CHECK(capacity >= 0 && nsym, IVC_E_ARG, "intra_symbols: need capacity >= 0 and nsym");
+  QTab t;
+  TRY(load_table(table, &t));
+  Staging st;
+  TRY(st.open());
+  const void* d_img = st.in(img, (size_t)(nframes * H * W * C));
+  int64_t* d_n = (int64_t*)st.alloc(8);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_intra_symbols(d_img, dtype, nframes, H, W, C, t, eob, nullptr, 0, d_n,
+                                       st.ctx->stream), "intra_symbols"));
+  int64_t total = 0;
+  TRY(st.out(&total, d_n, 8));
+  TRY(st.sync());
+  *nsym = total;
+  if (total > capacity)
+    return fail(IVC_E_SHAPE, "intra_symbols: the stream holds " + std::to_string(total) +
+                                 " symbols, more than capacity " + std::to_string(capacity));
+  int32_t* d_out = (int32_t*)st.alloc((size_t)total * 4);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_intra_symbols(d_img, dtype, nframes, H, W, C, t, eob, d_out, total, d_n,
+                                       st.ctx->stream), "intra_symbols"));
+  TRY(st.out(out, d_out, (size_t)total * 4));
+  return st.sync();
+}
+
 int ivc_minmax_i32_dev(const int32_t* sym, int64_t n, int32_t* mm, void* stream) {
   CHECK(n >= 0 && mm, IVC_E_ARG, "minmax: need n >= 0 and an output");
   return dev_launch(launch_minmax_i32(sym, n, mm, (hipStream_t)stream), "minmax");

@@ -255,6 +255,14 @@ hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, 
   return device_scan<int64_t>(nblk, CountGen{counts}, SumI64{}, OffsetSink{off, nblk}, agg, s);
 }
 
+// off[0..n] = exclusive int64 prefix of counts[0..n), off[n] = total (agg: scratch of
+// scan_scratch_elems(n) int64)
+hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* agg, int64_t* off,
+                                     hipStream_t s) {
+  if (n <= 0) return hipMemsetAsync(off, 0, sizeof(int64_t), s);
+  return device_scan<int64_t>(n, CountGen{counts}, SumI64{}, OffsetSink{off, n}, agg, s);
+}
+
 // symbols of every block at its offset; symbols at or past `capacity` are not written
 hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
                                const int64_t* off, int32_t* out, int64_t capacity, hipStream_t s) {

@@ -41,6 +41,11 @@ hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, in
 unsigned resident_grid_ptr(const void* kernel, int64_t work_groups_needed);
 // zero-run coding (ivc_entropy.hip)
 int64_t scan_scratch_elems(int64_t n);
+hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* agg, int64_t* off,
+                                     hipStream_t s);
+hipError_t launch_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
+                                int C, const QTab& t, int32_t eob, int32_t* out, int64_t capacity,
+                                int64_t* nsym, hipStream_t s);
 hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, int B,
                                   int32_t* counts, int64_t* agg, int64_t* off, hipStream_t s);
 hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,

@@ -329,6 +329,13 @@ struct FusedArgs {
   int sr;
   int dup12;             // table planes 1 and 2 identical (always true for PatchQuant tables);
                          // C = 1 kernels take it as the template flag DUP
+  // zero-run symbol modes (OUTM = OUT_COUNT / OUT_SYMBOLS): per-group symbol counts, their
+  // exclusive offsets, the int32 stream and its capacity, the EOB symbol
+  int32_t* zr_counts;
+  const int64_t* zr_off;
+  int32_t* zr_out;
+  int64_t zr_cap;
+  int32_t zr_eob;
 #ifdef IVC_ABLATION
   int ablate;            // diagnostic builds only (tools/ablate): bit mask of skipped phases
 #endif
@@ -546,12 +553,19 @@ __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* o
   }
 }
 
-// Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging.
+// Output modes of the fused kernel: the quantised blocks themselves (OUT_COEFS: staged in LDS
+// and stored), or the blocks' zero-run symbols (ivclab/entropy/zerorun.py:10-43) — their
+// per-group counts (OUT_COUNT) or the symbol stream at scanned offsets (OUT_SYMBOLS).
+enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2 };
+
+// Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging
+// (OUT_COEFS) or into qs[plane][row] (symbol modes; plane 2 of a DUP table is plane 1).
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
-          bool DUP>
+          bool DUP, int OUTM = OUT_COEFS>
 __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI, C, SRC>& v,
                                              T* xs, int32_t* os, const double* srq, const D* sq,
-                                             int b, int r, uint32_t zp0, uint32_t zp1) {
+                                             int b, int r, uint32_t zp0, uint32_t zp1,
+                                             int32_t (&qs)[3][8]) {
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     // ---- row pass (axis -1): lane owns row r of block b ------------------------------------
@@ -606,9 +620,13 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
       auto pos_of = [&](int i) {
         return ZZ ? (int)(((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u) : i * 8 + r;
       };
+      auto put = [&](int i, int32_t q) {
+        if constexpr (OUTM == OUT_COEFS) ob[pos_of(i)] = q;
+        else qs[p][i] = q;
+      };
       if (IVC_SKIP(a, 4)) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) ob[pos_of(i)] = (int)x[i];
+        for (int i = 0; i < 8; ++i) put(i, (int)x[i]);
       } else if constexpr (FAST) {
         // quotient via the scaled reciprocal, staged at once; values within 2^-30 of a
         // rounding boundary (or too large to bound the error) are redone below by exact
@@ -621,7 +639,7 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
           bool ok = __builtin_fabs(yq - rr) < 0.5 - 0x1p-30;
           if (CHECKMAG) ok = ok && __builtin_fabs(yq) < 0x1p20;
           all_ok = all_ok && ok;
-          ob[pos_of(i)] = (int)rr;
+          put(i, (int)rr);
         }
         if (__ballot(!all_ok)) {
 #pragma unroll
@@ -632,23 +650,96 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
             if (CHECKMAG) ok = ok && __builtin_fabs(yq) < 0x1p20;
             if (!ok) {
               const double Y = x[i] * (dct2_scale(i) * dct2_scale(r));
-              ob[pos_of(i)] = np_to_i32<double>(__builtin_rint(Y / (double)sq[p * 64 + i * 8 + r]));
+              put(i, np_to_i32<double>(__builtin_rint(Y / (double)sq[p * 64 + i * 8 + r])));
             }
           }
         }
       } else {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-          ob[pos_of(i)] = np_to_i32<D>(rint_t<D>((D)x[i] / sq[p * 64 + i * 8 + r]));
+          put(i, np_to_i32<D>(rint_t<D>((D)x[i] / sq[p * 64 + i * 8 + r])));
       }
     }
     __builtin_amdgcn_wave_barrier();
   }
 }
 
+// Zero-run coding of the group's 8 blocks x 3 planes straight from the quantised values in
+// registers (lane (b, r) holds zig-zag positions zpos(i) of column r).  A block's nonzero
+// mask is the OR of its 8 lanes' bits; its symbol count and every coefficient's slot follow
+// from the mask alone (same rules as ivc_entropy.hip's zr_mask).  Stream order is the
+// reference's (h w c): block-major, planes inside a block.
+template <int C, bool DUP, int OUTM>
+__device__ __forceinline__ void zr_group(const FusedArgs& a, const int32_t (&qs)[3][8], int b, int r,
+                                         uint32_t zp0, uint32_t zp1, int nb, int64_t gid) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes held in qs
+  const bool live = b < nb;
+  uint64_t m[NP], st[NP];
+  int cnt[NP];
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    uint64_t lm = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t z = ((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u;
+      lm |= (uint64_t)(live && qs[p][i] != 0) << z;
+    }
+    lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 1);
+    lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 2);
+    lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 4);
+    const int last = lm ? 63 - __builtin_clzll(lm) : -1;
+    const uint64_t inside = last < 0 ? 0ull : (last == 63 ? ~0ull : ((1ull << (last + 1)) - 1));
+    const uint64_t zeros = ~lm & inside;
+    m[p] = lm;
+    st[p] = zeros & ~(zeros << 1);
+    cnt[p] = live ? __builtin_popcountll(lm) + 2 * __builtin_popcountll(st[p]) + 1 : 0;
+  }
+  const int c2 = NP == 2 ? cnt[1] : cnt[NP - 1];
+  const int tb = cnt[0] + cnt[1] + c2;                       // the block's symbols
+  if constexpr (OUTM == OUT_COUNT) {
+    int v = r == 0 ? tb : 0;
+#pragma unroll
+    for (int d = 8; d < 64; d <<= 1) v += __shfl_xor(v, d);
+    if ((threadIdx.x & 63) == 0) a.zr_counts[gid] = v;
+  } else {
+    // exclusive prefix of the block totals over b (lane groups of 8)
+    int inc = tb;
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 8; d < 64; d <<= 1) {
+      const int o = __shfl_up(inc, d);
+      if (lane >= d) inc += o;
+    }
+    const int64_t base = a.zr_off[gid] + (inc - tb);
+    const int64_t pb[3] = {base, base + cnt[0], base + cnt[0] + cnt[1]};
+#pragma unroll
+    for (int pp = 0; pp < 3; ++pp) {
+      const int p = pp < NP ? pp : NP - 1;
+      const int64_t bp = pb[pp];
+      if (!live) continue;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t z = ((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u;
+        const uint64_t bit = 1ull << z, below = bit - 1;
+        const int64_t pos = bp + __builtin_popcountll(m[p] & below) +
+                            2 * __builtin_popcountll(st[p] & below);
+        if (m[p] & bit) {
+          if (pos < a.zr_cap) a.zr_out[pos] = qs[p][i];
+        } else if (st[p] & bit) {
+          if (pos < a.zr_cap) a.zr_out[pos] = 0;
+          if (pos + 1 < a.zr_cap) a.zr_out[pos + 1] = __builtin_ctzll(m[p] >> z);
+        }
+      }
+      const int64_t e = bp + cnt[p] - 1;
+      if (r == 0 && e < a.zr_cap) a.zr_out[e] = a.zr_eob;
+    }
+  }
+}
+
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
-          int NG, bool DUP>
+          int NG, bool DUP, int OUTM = OUT_COEFS>
 __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) {
+  static_assert(OUTM == OUT_COEFS || (ZZ && SRC == SRC_IMAGE), "symbols need zig-zag order");
   typedef WaveLds<T, C, DUP> L;
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
   __shared__ double srq[FAST ? 192 : 1];
@@ -685,10 +776,13 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
   // compiler's vmcnt wait never includes the stores.  Ragged / non-existent groups go
   // through zero-range descriptors instead of branches.
   TileRaw<TI, C, NG> raw;
+  int32_t qs[3][8];
   if constexpr (SRC == SRC_IMAGE) {
     load_tile<TI, C, NG>(a, lt, lt < nlt, lane, raw);
+    if constexpr (OUTM == OUT_COEFS) {
 #pragma unroll
-    for (int g = 1; g < NG; ++g) store_group<NG, C, DUP>(a, os, lane, 0u, 0, false);
+      for (int g = 1; g < NG; ++g) store_group<NG, C, DUP>(a, os, lane, 0u, 0, false);
+    }
   }
   uint32_t plt = 0;
   int pg = 0;
@@ -697,7 +791,8 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
     TileRaw<TI, C, NG> nraw;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
-      store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+      if constexpr (OUTM == OUT_COEFS)
+        store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
       RowReg<TI, C, SRC> v;
       if constexpr (SRC == SRC_IMAGE) {
         if (g == 0) {
@@ -708,14 +803,19 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
       } else {
         gather_inter(a, lt, b, r, v);
       }
-      encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+      encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM>(a, v, xs, os, srq, sq, b, r,
+                                                                    zp0, zp1, qs);
+      if constexpr (OUTM != OUT_COEFS)
+        zr_group<C, DUP, OUTM>(a, qs, b, r, zp0, zp1, group_loc<NG>(a, lt, g).nb,
+                               (int64_t)lt * NG + g);
       plt = lt;
       pg = g;
       have_prev = true;
     }
     if constexpr (SRC == SRC_IMAGE) raw = nraw;
   }
-  store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+  if constexpr (OUTM == OUT_COEFS)
+    store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
 }
 
 
@@ -758,14 +858,15 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
   const int64_t nlt = (int64_t)a.nframes * a.h * a.tpr;
   // IVC_FUSED_GRID: 0 = exactly resident (persistent waves), k > 0 = k tiles per wave
   auto grid = [&](auto k) -> unsigned {
-    if (IVC_FUSED_GRID == 0) {
+    if constexpr (IVC_FUSED_GRID == 0) {
       unsigned g = resident_grid(k, (nlt + 3) / 4);
       if (IVC_FUSED_WGCU > 0 && g > (unsigned)(num_cus() * IVC_FUSED_WGCU))
         g = (unsigned)(num_cus() * IVC_FUSED_WGCU);
       return g;
+    } else {
+      const int64_t g = (nlt + 4 * IVC_FUSED_GRID - 1) / (4 * IVC_FUSED_GRID);
+      return (unsigned)(g < 1 ? 1 : g);
     }
-    const int64_t g = (nlt + 4 * IVC_FUSED_GRID - 1) / (4 * IVC_FUSED_GRID);
-    return (unsigned)(g < 1 ? 1 : g);
   };
   if (C == 1 && a.dup12) {
     auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, C == 1>;
@@ -806,6 +907,11 @@ static FusedArgs make_fused_args(const void* img, const int64_t* mv, int32_t* ou
   a.H = (int)H; a.W = (int)W; a.h = (int)(H / 8); a.w = (int)(W / 8);
   a.tpr = (a.w + 7) / 8;
   a.sr = sr;
+  a.zr_counts = nullptr;
+  a.zr_off = nullptr;
+  a.zr_out = nullptr;
+  a.zr_cap = 0;
+  a.zr_eob = 0;
   a.dup12 = 1;
   for (int i = 0; i < 64; ++i)
     if (t.q[64 + i] != t.q[128 + i]) a.dup12 = 0;
@@ -847,6 +953,69 @@ hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int6
       return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+// ---- pixels -> zero-run symbols (IntraCodec.image2symbols' hot part, intracodec.py:66-81):
+// count pass, int64 scan of the per-group counts, emission pass.
+template <typename TI, int C, bool DUP, bool CM, int OUTM>
+static void launch_fused_zr(const FusedArgs& a_in, const QTab& t, hipStream_t s) {
+  constexpr int NG = (sizeof(TI) == 1 && C == 1) ? IVC_WIDE_NG : 1;
+  FusedArgs a = a_in;
+  a.tpr = (a.w + 8 * NG - 1) / (8 * NG);
+  const int64_t nlt = (int64_t)a.nframes * a.h * a.tpr;
+  auto k = fused_encode_kernel<TI, double, double, C, true, true, SRC_IMAGE, CM, NG, DUP, OUTM>;
+  k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
+}
+
+template <typename TI, int C, bool DUP, bool CM>
+static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* nsym,
+                                  hipStream_t s) {
+  constexpr int NG = (sizeof(TI) == 1 && C == 1) ? IVC_WIDE_NG : 1;
+  const int64_t tpr = (a0.w + 8 * NG - 1) / (8 * NG);
+  const int64_t ngroups = (int64_t)a0.nframes * a0.h * tpr * NG;
+  FusedArgs a = a0;
+  int32_t* counts = nullptr;
+  int64_t* agg = nullptr;
+  int64_t* off = nullptr;
+  hipError_t e = hipMallocAsync((void**)&counts, (size_t)ngroups * 4, s);
+  if (e == hipSuccess) e = hipMallocAsync((void**)&agg, (size_t)scan_scratch_elems(ngroups) * 8, s);
+  if (e == hipSuccess) e = hipMallocAsync((void**)&off, (size_t)(ngroups + 1) * 8, s);
+  if (e == hipSuccess) {
+    a.zr_counts = counts;
+    a.zr_off = off;
+    launch_fused_zr<TI, C, DUP, CM, OUT_COUNT>(a, t, s);
+    e = launch_exclusive_scan_i32(counts, ngroups, agg, off, s);
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(nsym, off + ngroups, 8, hipMemcpyDeviceToDevice, s);
+  if (e == hipSuccess && a.zr_cap > 0) {
+    launch_fused_zr<TI, C, DUP, CM, OUT_SYMBOLS>(a, t, s);
+    e = hipGetLastError();
+  }
+  if (counts) (void)hipFreeAsync(counts, s);
+  if (agg) (void)hipFreeAsync(agg, s);
+  if (off) (void)hipFreeAsync(off, s);
+  return e;
+}
+
+hipError_t launch_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
+                                int C, const QTab& t, int32_t eob, int32_t* out, int64_t capacity,
+                                int64_t* nsym, hipStream_t s) {
+  if (dtype != IVC_U8 || (C != 1 && C != 3)) return hipErrorInvalidValue;
+  FusedArgs a = make_fused_args(img, nullptr, nullptr, nframes, H, W, 0, t);
+  a.zr_out = out;
+  a.zr_cap = capacity;
+  a.zr_eob = eob;
+  if (nframes <= 0 || H <= 0 || W <= 0) return hipMemsetAsync(nsym, 0, 8, s);
+  if (nframes * (int64_t)a.h * a.tpr >= (1LL << 31)) return hipErrorInvalidValue;
+  const bool cm = needs_magnitude_check(t);
+  if (C == 1) {
+    if (a.dup12) return cm ? intra_symbols_t<uint8_t, 1, true, true>(a, t, nsym, s)
+                           : intra_symbols_t<uint8_t, 1, true, false>(a, t, nsym, s);
+    return cm ? intra_symbols_t<uint8_t, 1, false, true>(a, t, nsym, s)
+              : intra_symbols_t<uint8_t, 1, false, false>(a, t, nsym, s);
+  }
+  return cm ? intra_symbols_t<uint8_t, 3, false, true>(a, t, nsym, s)
+            : intra_symbols_t<uint8_t, 3, false, false>(a, t, nsym, s);
 }
 
 hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W,

@@ -135,3 +135,20 @@ def minmax(sym, mm, stream=None):
         raise ValueError("minmax: int32 symbols and an int32 output of 2")
     N.check(N.lib().ivc_minmax_i32_dev(sym.data_ptr(), sym.numel(), mm.data_ptr(),
                                        _stream(stream)), "minmax")
+
+
+def intra_symbols(frames, table, out, nsym, eob=4000, stream=None):
+    """u8 frames [F, H, W] or [F, H, W, C] -> the zero-run symbol stream of their quantised
+    zig-zag blocks (IntraCodec.image2symbols without colour conversion, one fused pass per
+    frame batch; the coefficients never reach memory).  out: int32 (written up to its
+    length), nsym: int64 device scalar receiving the stream length.  Asynchronous."""
+    import torch
+    _contig(frames, "frames"); _contig(out, "out"); _contig(nsym, "nsym")
+    if frames.dtype != torch.uint8 or out.dtype != torch.int32 or nsym.dtype != torch.int64:
+        raise ValueError("intra_symbols: uint8 frames, int32 out, int64 nsym")
+    F, H, W = frames.shape[:3]
+    C = frames.shape[3] if frames.dim() == 4 else 1
+    t = N.table_arg(table)
+    N.check(N.lib().ivc_intra_symbols_dev(frames.data_ptr(), N.DTYPE_CODE[np.dtype(np.uint8)], F, H,
+                                          W, C, N.ptr(t), int(eob), out.data_ptr(), out.numel(),
+                                          nsym.data_ptr(), _stream(stream)), "intra_symbols")

@@ -569,3 +569,68 @@ def test_minmax_host_and_device():
         dm = torch.zeros(2, dtype=torch.int32, device="cuda")
         D.minmax(t, dm)
         assert dm.cpu().tolist() == list(map(int, want))
+
+
+def _zr_chain(img, table, scale=None):
+    """Oracle chain: per frame zero-run(zig-zag(quantize(dct(patch)))) concatenated."""
+    out = []
+    for f in range(img.shape[0]):
+        d = O.dct_transform(O.patch(img[f]))
+        q = np.round(d / table[None, None]).astype(np.int32)
+        out.append(O.zerorun_encode_fast(O.zigzag_flatten(q)))
+    return np.concatenate(out) if out else np.zeros(0, np.int32)
+
+
+@pytest.mark.parametrize("case", ["s1", "s05", "s007", "custom", "rgb", "ragged"])
+def test_intra_symbols_fused_vs_oracle(case):
+    """Pixels -> zero-run symbols in one fused pass against the oracle's per-op chain."""
+    N, L = _native()
+    rng = np.random.default_rng(hash(case) % 1000)
+    F, H, W, C = 2, 48, 128, 1
+    scale = {"s1": 1.0, "s05": 0.5, "s007": 0.07}.get(case, 1.0)
+    if case == "rgb":
+        C = 3
+    if case == "ragged":
+        W = 264                                     # 33 blocks: the last group holds 1 block
+    img = rng.integers(0, 256, (F, H, W, C), dtype=np.uint8)
+    img[:, :16] = img[:, :1, :1]                    # flat blocks: all-zero AC, EOB-only planes
+    img[:, 16:24] = np.arange(W, dtype=np.uint8)[None, None, :, None] // 3
+    table = PatchQuant(scale).get_quantization_table().astype(np.float64)
+    if case == "custom":
+        table[2] *= 1.61                            # planes 1 and 2 differ
+    want = _zr_chain(img, table)
+    cap = want.size + 5
+    out = np.full(cap, -7, np.int32)
+    nsym = np.zeros(1, np.int64)
+    N.check(L.ivc_intra_symbols(N.ptr(img), 1, F, H, W, C, N.ptr(N.table_arg(table)), 4000,
+                                N.ptr(out), cap, N.ptr(nsym)))
+    assert int(nsym[0]) == want.size
+    assert_bits(out[:want.size], want, case)
+    # too small a buffer: an error that reports the needed length
+    with pytest.raises(ValueError):
+        N.check(L.ivc_intra_symbols(N.ptr(img), 1, F, H, W, C, N.ptr(N.table_arg(table)), 4000,
+                                    N.ptr(out), want.size - 1, N.ptr(nsym)))
+    assert int(nsym[0]) == want.size
+
+
+def test_intra_symbols_device_and_4k():
+    """Device API on a full 4K luma frame pair, and a capacity-limited prefix."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(4096)
+    img = rng.integers(0, 256, (2, 2160, 3840), dtype=np.uint8)
+    img[0, :800] = 90
+    table = PatchQuant(1.0).get_quantization_table()
+    want = _zr_chain(img[..., None], table.astype(np.float64))
+    fr = torch.from_numpy(img).cuda()
+    nsym = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out = torch.empty(want.size, dtype=torch.int32, device="cuda")
+    D.intra_symbols(fr, table, out, nsym)
+    torch.cuda.synchronize()
+    assert int(nsym.item()) == want.size
+    assert np.array_equal(out.cpu().numpy(), want)
+    short = torch.full((12345,), -1, dtype=torch.int32, device="cuda")
+    D.intra_symbols(fr, table, short, nsym)
+    torch.cuda.synchronize()
+    assert int(nsym.item()) == want.size
+    assert np.array_equal(short.cpu().numpy(), want[:12345])
