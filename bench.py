@@ -248,6 +248,10 @@ def main():
     nsym = int(offs[-1].item())
     sym = torch.empty(nsym, dtype=torch.int32, device=dev)
     zwall, zms = timed(dist, lambda: D.zerorun_encode(blocks, offs, sym), 3, 1)
+    # the same stream straight from the pixels (fused: the coefficients never reach HBM)
+    nsym_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    fwall, fms = timed(dist, lambda: D.intra_symbols(frames, table, sym, nsym_d), 3, 1)
+    fused_same = bool(int(nsym_d.item()) == nsym)
     mm = torch.empty(2, dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
     t_ex = time.perf_counter()
@@ -296,6 +300,12 @@ def main():
                     "ms": round(zms, 3), "Mblocks_per_s": round(nblk / zms / 1e3, 1),
                     "note": "ZeroRunCoder.encode of the zig-zag output (count, scan, emit kernels)",
                     "algorithmic_GBs": round((nblk * 256 + nsym * 4) / (zms * 1e-3) / 1e9, 1)},
+        "image2symbols": {"ms": round(fms, 3), "Mpixels_per_s": round(px_step / fms / 1e3, 1),
+                          "same_length_as_two_step": fused_same,
+                          "note": "u8 pixels -> DCT -> quant -> zig-zag -> zero-run symbols fused "
+                                  "(count pass + scan + emit pass; 2 x 1 B/px read, 4 B/symbol "
+                                  "written)",
+                          "algorithmic_GBs": round((px_step + nsym * 4) / (fms * 1e-3) / 1e9, 1)},
         "exchange": {"alphabet": [b0, b1], "bins": b1 - b0 - 1, "symbols": total_syms,
                      "entropy_bits_per_symbol": round(entropy_bits(pmf), 4),
                      "ms": round(exchange_ms, 3),

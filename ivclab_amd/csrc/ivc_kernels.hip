@@ -558,14 +558,12 @@ __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* o
 // per-group counts (OUT_COUNT) or the symbol stream at scanned offsets (OUT_SYMBOLS).
 enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2 };
 
-// Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging
-// (OUT_COEFS) or into qs[plane][row] (symbol modes; plane 2 of a DUP table is plane 1).
+// Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging.
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
-          bool DUP, int OUTM = OUT_COEFS>
+          bool DUP>
 __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI, C, SRC>& v,
                                              T* xs, int32_t* os, const double* srq, const D* sq,
-                                             int b, int r, uint32_t zp0, uint32_t zp1,
-                                             int32_t (&qs)[3][8]) {
+                                             int b, int r, uint32_t zp0, uint32_t zp1) {
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     // ---- row pass (axis -1): lane owns row r of block b ------------------------------------
@@ -620,10 +618,7 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
       auto pos_of = [&](int i) {
         return ZZ ? (int)(((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u) : i * 8 + r;
       };
-      auto put = [&](int i, int32_t q) {
-        if constexpr (OUTM == OUT_COEFS) ob[pos_of(i)] = q;
-        else qs[p][i] = q;
-      };
+      auto put = [&](int i, int32_t q) { ob[pos_of(i)] = q; };
       if (IVC_SKIP(a, 4)) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) put(i, (int)x[i]);
@@ -664,26 +659,36 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
   }
 }
 
-// Zero-run coding of the group's 8 blocks x 3 planes straight from the quantised values in
-// registers (lane (b, r) holds zig-zag positions zpos(i) of column r).  A block's nonzero
-// mask is the OR of its 8 lanes' bits; its symbol count and every coefficient's slot follow
-// from the mask alone (same rules as ivc_entropy.hip's zr_mask).  Stream order is the
-// reference's (h w c): block-major, planes inside a block.
+// Zero-run coding of the group's 8 blocks x 3 planes from the zig-zag staging in LDS (the
+// same staging OUT_COEFS stores).  Lane (b, r) takes zig-zag positions 8r .. 8r+7 of block
+// b: a block's nonzero mask is the OR of its 8 lanes' bytes; its symbol count and each
+// lane's first output slot follow from the mask, and the lane walks its 8 coefficients in
+// stream order (same rules as ivc_entropy.hip's zr_mask).  Stream order is the reference's
+// (h w c): block-major, planes inside a block.  OUT_SYMBOLS assembles the group's stream in
+// the wave's LDS region, ZR_WIN symbols at a time, and stores it with whole-wave
+// consecutive dword stores.
+constexpr int ZR_WIN = XS_PITCH * 8 * 8 / 4;   // int32 symbols in a wave's transpose region
+
 template <int C, bool DUP, int OUTM>
-__device__ __forceinline__ void zr_group(const FusedArgs& a, const int32_t (&qs)[3][8], int b, int r,
-                                         uint32_t zp0, uint32_t zp1, int nb, int64_t gid) {
-  constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes held in qs
+__device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b, int r, int nb,
+                                         int64_t gid) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging
+  constexpr int PITCH = os_pitch<C, DUP>();
   const bool live = b < nb;
+  const int lane = threadIdx.x & 63;
+  int32_t val[NP][8];
   uint64_t m[NP], st[NP];
   int cnt[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
-    uint64_t lm = 0;
+    const int4* src = reinterpret_cast<const int4*>(os + b * PITCH + p * 64 + 8 * r);
+    const int4 v0 = src[0], v1 = src[1];
+    val[p][0] = v0.x; val[p][1] = v0.y; val[p][2] = v0.z; val[p][3] = v0.w;
+    val[p][4] = v1.x; val[p][5] = v1.y; val[p][6] = v1.z; val[p][7] = v1.w;
+    uint32_t byte = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t z = ((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u;
-      lm |= (uint64_t)(live && qs[p][i] != 0) << z;
-    }
+    for (int k = 0; k < 8; ++k) byte |= (uint32_t)(val[p][k] != 0) << k;
+    uint64_t lm = live ? (uint64_t)byte << (8 * r) : 0ull;
     lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 1);
     lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 2);
     lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 4);
@@ -694,44 +699,70 @@ __device__ __forceinline__ void zr_group(const FusedArgs& a, const int32_t (&qs)
     st[p] = zeros & ~(zeros << 1);
     cnt[p] = live ? __builtin_popcountll(lm) + 2 * __builtin_popcountll(st[p]) + 1 : 0;
   }
-  const int c2 = NP == 2 ? cnt[1] : cnt[NP - 1];
+  __builtin_amdgcn_wave_barrier();                            // staging read: region free
+  const int c2 = cnt[NP - 1];
   const int tb = cnt[0] + cnt[1] + c2;                       // the block's symbols
   if constexpr (OUTM == OUT_COUNT) {
     int v = r == 0 ? tb : 0;
 #pragma unroll
     for (int d = 8; d < 64; d <<= 1) v += __shfl_xor(v, d);
-    if ((threadIdx.x & 63) == 0) a.zr_counts[gid] = v;
+    if (lane == 0) a.zr_counts[gid] = v;
   } else {
     // exclusive prefix of the block totals over b (lane groups of 8)
     int inc = tb;
-    const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int d = 8; d < 64; d <<= 1) {
       const int o = __shfl_up(inc, d);
       if (lane >= d) inc += o;
     }
-    const int64_t base = a.zr_off[gid] + (inc - tb);
-    const int64_t pb[3] = {base, base + cnt[0], base + cnt[0] + cnt[1]};
+    const int pre = inc - tb;                                 // symbols of blocks before b
+    const int gtot = __shfl(inc, 56);                         // the group's symbols
+    const int64_t gbase = a.zr_off[gid];
+    // each lane's first slot per plane: symbols of the block's zig-zag positions < 8r
+    const uint64_t low = r == 0 ? 0ull : (~0ull >> (64 - 8 * r));
+    int first[3];
+    {
+      int pb = pre;
 #pragma unroll
-    for (int pp = 0; pp < 3; ++pp) {
-      const int p = pp < NP ? pp : NP - 1;
-      const int64_t bp = pb[pp];
-      if (!live) continue;
+      for (int pp = 0; pp < 3; ++pp) {
+        const int p = pp < NP ? pp : NP - 1;
+        first[pp] = pb + __builtin_popcountll(m[p] & low) + 2 * __builtin_popcountll(st[p] & low);
+        pb += cnt[p];
+      }
+    }
+    int32_t* zs = os;                                         // staging consumed above
+    for (int w0 = 0; w0 < gtot; w0 += ZR_WIN) {
+      auto put = [&](int pos, int32_t v) {
+        const unsigned o = (unsigned)(pos - w0);
+        if (o < (unsigned)ZR_WIN) zs[o] = v;
+      };
+      if (live) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t z = ((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u;
-        const uint64_t bit = 1ull << z, below = bit - 1;
-        const int64_t pos = bp + __builtin_popcountll(m[p] & below) +
-                            2 * __builtin_popcountll(st[p] & below);
-        if (m[p] & bit) {
-          if (pos < a.zr_cap) a.zr_out[pos] = qs[p][i];
-        } else if (st[p] & bit) {
-          if (pos < a.zr_cap) a.zr_out[pos] = 0;
-          if (pos + 1 < a.zr_cap) a.zr_out[pos + 1] = __builtin_ctzll(m[p] >> z);
+        for (int pp = 0; pp < 3; ++pp) {
+          const int p = pp < NP ? pp : NP - 1;
+          const uint32_t mb = (uint32_t)(m[p] >> (8 * r)) & 0xffu;
+          const uint32_t sb = (uint32_t)(st[p] >> (8 * r)) & 0xffu;
+          int pos = first[pp];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            if ((mb >> k) & 1u) {
+              put(pos, val[p][k]);
+              pos += 1;
+            } else if ((sb >> k) & 1u) {
+              put(pos, 0);
+              put(pos + 1, __builtin_ctzll(m[p] >> (8 * r + k)));
+              pos += 2;
+            }
+          }
+          if (r == 0) put(first[pp] + cnt[p] - 1, a.zr_eob);     // r = 0: first = plane start
         }
       }
-      const int64_t e = bp + cnt[p] - 1;
-      if (r == 0 && e < a.zr_cap) a.zr_out[e] = a.zr_eob;
+      __builtin_amdgcn_wave_barrier();
+      const int n = gtot - w0 < ZR_WIN ? gtot - w0 : ZR_WIN;
+      const int64_t dst = gbase + w0;
+      for (int j = lane; j < n; j += 64)
+        if (dst + j < a.zr_cap) a.zr_out[dst + j] = zs[j];
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
@@ -776,7 +807,6 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
   // compiler's vmcnt wait never includes the stores.  Ragged / non-existent groups go
   // through zero-range descriptors instead of branches.
   TileRaw<TI, C, NG> raw;
-  int32_t qs[3][8];
   if constexpr (SRC == SRC_IMAGE) {
     load_tile<TI, C, NG>(a, lt, lt < nlt, lane, raw);
     if constexpr (OUTM == OUT_COEFS) {
@@ -803,11 +833,9 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
       } else {
         gather_inter(a, lt, b, r, v);
       }
-      encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM>(a, v, xs, os, srq, sq, b, r,
-                                                                    zp0, zp1, qs);
+      encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
       if constexpr (OUTM != OUT_COEFS)
-        zr_group<C, DUP, OUTM>(a, qs, b, r, zp0, zp1, group_loc<NG>(a, lt, g).nb,
-                               (int64_t)lt * NG + g);
+        zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, lt, g).nb, (int64_t)lt * NG + g);
       plt = lt;
       pg = g;
       have_prev = true;
