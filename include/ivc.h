@@ -168,6 +168,22 @@ int ivc_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, 
 int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
                           int64_t* hist, void* stream);
 
+/* ---------------------------------------------------------------- colour ----------- */
+/* rgb2ycbcr (ivclab/signal/color.py:15-38): npix pixels of 3 channels (any dtype) ->
+ * float64 YCbCr, NumPy's `image @ M.T + offset` bit for bit (OpenBLAS dgemm k-order FMA).  */
+int ivc_rgb2ycbcr(const void* src, int src_dtype, int64_t npix, double* dst);
+int ivc_rgb2ycbcr_dev(const void* src, int src_dtype, int64_t npix, double* dst, void* stream);
+/* ycbcr2rgb (color.py:40-63): channels 0..2 of npix pixels of `channels` (>= 3) values ->
+ * clipped RGB, float32 for float32 input, float64 otherwise.                               */
+int ivc_ycbcr2rgb(const void* src, int src_dtype, int64_t npix, int64_t channels, void* dst);
+int ivc_ycbcr2rgb_dev(const void* src, int src_dtype, int64_t npix, int64_t channels, void* dst,
+                      void* stream);
+/* rgb2gray (color.py:3-13): mean over the `channels` (1..7) values of each pixel, float32
+ * for float32 input, float64 otherwise.                                                    */
+int ivc_rgb2gray(const void* src, int src_dtype, int64_t npix, int64_t channels, void* dst);
+int ivc_rgb2gray_dev(const void* src, int src_dtype, int64_t npix, int64_t channels, void* dst,
+                     void* stream);
+
 /* ---------------------------------------------------------------- zero-run coding -- */
 /* ZeroRunCoder.encode (ivclab/entropy/zerorun.py:10-43): src holds nblk rows of row_stride
  * int32 coefficients in (h w c) order; the first block_size (0..64, <= row_stride) of each

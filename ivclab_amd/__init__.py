@@ -32,6 +32,7 @@ _ALIASES = {
     "ivclab.signal": "ivclab_amd.signal",
     "ivclab.signal.dct": "ivclab_amd.signal.dct",
     "ivclab.signal.zigzag": "ivclab_amd.signal.zigzag",
+    "ivclab.signal.color": "ivclab_amd.signal.color",
     "ivclab.quantization": "ivclab_amd.quantization",
     "ivclab.quantization.patchquant": "ivclab_amd.quantization.patchquant",
     "ivclab.utils": "ivclab_amd.utils",

@@ -62,6 +62,12 @@ _SIGS = {
     "ivc_histogram_i32": ([_P, _L, _ct.c_int32, _ct.c_int32, _P], _I),
     "ivc_histogram_i32_dev": ([_P, _L, _ct.c_int32, _ct.c_int32, _P, _P], _I),
     "ivc_histogram_i64": ([_P, _L, _L, _ct.c_int32, _P], _I),
+    "ivc_rgb2ycbcr": ([_P, _ct.c_int, _L, _P], _I),
+    "ivc_rgb2ycbcr_dev": ([_P, _ct.c_int, _L, _P, _P], _I),
+    "ivc_ycbcr2rgb": ([_P, _ct.c_int, _L, _L, _P], _I),
+    "ivc_ycbcr2rgb_dev": ([_P, _ct.c_int, _L, _L, _P, _P], _I),
+    "ivc_rgb2gray": ([_P, _ct.c_int, _L, _L, _P], _I),
+    "ivc_rgb2gray_dev": ([_P, _ct.c_int, _L, _L, _P, _P], _I),
     "ivc_intra_symbols": ([_P, _ct.c_int, _L, _L, _L, _ct.c_int, _P, _ct.c_int32, _P, _L, _P], _I),
     "ivc_intra_symbols_dev": ([_P, _ct.c_int, _L, _L, _L, _ct.c_int, _P, _ct.c_int32, _P, _L, _P, _P], _I),
     "ivc_minmax_i32": ([_P, _L, _P], _I),

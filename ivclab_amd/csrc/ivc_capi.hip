@@ -489,6 +489,74 @@ int ivc_histogram_i32(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, 
   return st.sync();
 }
 
+// ---------------------------------------------------------------- colour --------------
+static size_t color_out_size(int dtype) { return dtype == IVC_F32 ? 4 : 8; }
+
+int ivc_rgb2ycbcr_dev(const void* src, int src_dtype, int64_t npix, double* dst, void* stream) {
+  CHECK(valid_dtype(src_dtype), IVC_E_DTYPE, "rgb2ycbcr: unsupported dtype");
+  CHECK(npix >= 0, IVC_E_ARG, "rgb2ycbcr: negative size");
+  return dev_launch(launch_rgb2ycbcr(src, src_dtype, npix, dst, (hipStream_t)stream), "rgb2ycbcr");
+}
+
+int ivc_rgb2ycbcr(const void* src, int src_dtype, int64_t npix, double* dst) {
+  CHECK(valid_dtype(src_dtype), IVC_E_DTYPE, "rgb2ycbcr: unsupported dtype");
+  CHECK(npix >= 0, IVC_E_ARG, "rgb2ycbcr: negative size");
+  Staging st;
+  TRY(st.open());
+  const void* d_src = st.in(src, (size_t)npix * 3 * dtype_size(src_dtype));
+  double* d_dst = (double*)st.alloc((size_t)npix * 3 * 8);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_rgb2ycbcr(d_src, src_dtype, npix, d_dst, st.ctx->stream), "rgb2ycbcr"));
+  TRY(st.out(dst, d_dst, (size_t)npix * 3 * 8));
+  return st.sync();
+}
+
+int ivc_ycbcr2rgb_dev(const void* src, int src_dtype, int64_t npix, int64_t channels, void* dst,
+                      void* stream) {
+  CHECK(valid_dtype(src_dtype), IVC_E_DTYPE, "ycbcr2rgb: unsupported dtype");
+  CHECK(npix >= 0 && channels >= 3, IVC_E_SHAPE, "ycbcr2rgb: need >= 3 channels");
+  return dev_launch(launch_ycbcr2rgb(src, src_dtype, npix, channels, dst, (hipStream_t)stream),
+                    "ycbcr2rgb");
+}
+
+int ivc_ycbcr2rgb(const void* src, int src_dtype, int64_t npix, int64_t channels, void* dst) {
+  CHECK(valid_dtype(src_dtype), IVC_E_DTYPE, "ycbcr2rgb: unsupported dtype");
+  CHECK(npix >= 0 && channels >= 3, IVC_E_SHAPE, "ycbcr2rgb: need >= 3 channels");
+  Staging st;
+  TRY(st.open());
+  const void* d_src = st.in(src, (size_t)(npix * channels) * dtype_size(src_dtype));
+  const size_t ob = (size_t)npix * 3 * color_out_size(src_dtype);
+  void* d_dst = st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_ycbcr2rgb(d_src, src_dtype, npix, channels, d_dst, st.ctx->stream),
+                  "ycbcr2rgb"));
+  TRY(st.out(dst, d_dst, ob));
+  return st.sync();
+}
+
+int ivc_rgb2gray_dev(const void* src, int src_dtype, int64_t npix, int64_t channels, void* dst,
+                     void* stream) {
+  CHECK(valid_dtype(src_dtype), IVC_E_DTYPE, "rgb2gray: unsupported dtype");
+  CHECK(npix >= 0 && channels >= 1 && channels < 8, IVC_E_SHAPE, "rgb2gray: 1..7 channels");
+  return dev_launch(launch_rgb2gray(src, src_dtype, npix, (int)channels, dst, (hipStream_t)stream),
+                    "rgb2gray");
+}
+
+int ivc_rgb2gray(const void* src, int src_dtype, int64_t npix, int64_t channels, void* dst) {
+  CHECK(valid_dtype(src_dtype), IVC_E_DTYPE, "rgb2gray: unsupported dtype");
+  CHECK(npix >= 0 && channels >= 1 && channels < 8, IVC_E_SHAPE, "rgb2gray: 1..7 channels");
+  Staging st;
+  TRY(st.open());
+  const void* d_src = st.in(src, (size_t)(npix * channels) * dtype_size(src_dtype));
+  const size_t ob = (size_t)npix * color_out_size(src_dtype);
+  void* d_dst = st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_rgb2gray(d_src, src_dtype, npix, (int)channels, d_dst, st.ctx->stream),
+                  "rgb2gray"));
+  TRY(st.out(dst, d_dst, ob));
+  return st.sync();
+}
+
 // ---------------------------------------------------------------- zero-run coding -----
 static int check_zr(int64_t nblk, int32_t stride, int32_t B) {
   CHECK(nblk >= 0, IVC_E_ARG, "zerorun: nblk must be >= 0");

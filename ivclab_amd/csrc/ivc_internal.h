@@ -51,6 +51,10 @@ hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, 
 hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
                                const int64_t* off, int32_t* out, int64_t capacity, hipStream_t s);
 int64_t zr_decode_scratch_bytes(int64_t n);
+hipError_t launch_rgb2ycbcr(const void* src, int dtype, int64_t npix, double* dst, hipStream_t s);
+hipError_t launch_ycbcr2rgb(const void* src, int dtype, int64_t npix, int64_t cstride, void* dst,
+                            hipStream_t s);
+hipError_t launch_rgb2gray(const void* src, int dtype, int64_t npix, int C, void* dst, hipStream_t s);
 hipError_t launch_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm, hipStream_t s);
 hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected, int B,
                                  int32_t eob, int32_t* out, void* scratch, int64_t* err,

@@ -353,3 +353,49 @@ def smooth_pmf(pmf, epsilon=1e-9):
     pmf = pmf + epsilon
     pmf /= pmf.sum()
     return pmf
+
+
+# ---------------------------------------------------------------- colour ----------------
+YCC_M = np.array([[0.299, 0.587, 0.114], [-0.168736, -0.331264, 0.5],
+                  [0.5, -0.418688, -0.081312]])
+
+
+def rgb2ycbcr(image):
+    """color.py:15-38 — the same NumPy matmul (OpenBLAS dgemm) and offset add."""
+    return image @ YCC_M.T + np.array([0, 128, 128])
+
+
+def rgb2ycbcr_fma(image):
+    """The arithmetic the GPU kernel performs: per output channel
+    fma(b, M[c,2], fma(g, M[c,1], r * M[c,0])) + offset, written with exact float64
+    operations (an FMA is emulated as an error-free product + sum).  Equal to rgb2ycbcr on
+    OpenBLAS's k-order FMA kernels (checked in tests/test_oracle_golden.py)."""
+    x = np.asarray(image, dtype=np.float64)
+    out = np.empty(x.shape, np.float64)
+    from fractions import Fraction  # exact rational arithmetic: small inputs only
+    flat_in = x.reshape(-1, 3)
+    flat_out = out.reshape(-1, 3)
+    off = (0.0, 128.0, 128.0)
+    for i, (r, g, b) in enumerate(flat_in):
+        for c in range(3):
+            acc = float(Fraction(r) * Fraction(YCC_M[c, 0]))
+            acc = float(Fraction(g) * Fraction(YCC_M[c, 1]) + Fraction(acc))
+            acc = float(Fraction(b) * Fraction(YCC_M[c, 2]) + Fraction(acc))
+            flat_out[i, c] = acc + off[c]
+    return out
+
+
+def ycbcr2rgb(image):
+    """color.py:40-63."""
+    Y = image[:, :, 0]
+    Cb = image[:, :, 1] - 128.0
+    Cr = image[:, :, 2] - 128.0
+    R = Y + 1.402 * Cr
+    G = Y - 0.344136 * Cb - 0.714136 * Cr
+    B = Y + 1.772 * Cb
+    return np.clip(np.stack([R, G, B], axis=-1), 0, 255)
+
+
+def rgb2gray(image):
+    """color.py:3-13."""
+    return np.mean(image, axis=-1, keepdims=True)

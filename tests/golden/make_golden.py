@@ -16,6 +16,7 @@ Reference modules used (paths relative to /root/reference):
   ivclab/video/motion.py          MotionCompensator
   ivclab/entropy/zerorun.py       ZeroRunCoder (zerorun.npz; its own RNG stream, so the
                                   other fixtures are unchanged by its addition)
+  ivclab/signal/color.py          rgb2gray, rgb2ycbcr, ycbcr2rgb (color.npz; own RNG stream)
 """
 import contextlib
 import importlib.util
@@ -195,6 +196,7 @@ def main():
         p[f"rec{C}"] = DCT.inverse_transform(Q.dequantize(_quiet(sh_m.ZigZag().unflatten, p[f"zz{C}"])))
     np.savez_compressed(os.path.join(OUT, "intra.npz"), **p)
     make_zerorun(p)
+    make_color()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
@@ -261,6 +263,35 @@ def make_zerorun(intra):
         except Exception as e:  # noqa: BLE001  (the reference's exception is the fixture)
             z[f"err_{k}_exc"] = np.array(f"{type(e).__name__}: {e}")
     np.savez_compressed(os.path.join(OUT, "zerorun.npz"), **z)
+
+
+def make_color():
+    """Colour conversion fixtures (rgb2ycbcr goes through NumPy's matmul -> OpenBLAS: the
+    fixtures record this container's NumPy 2.2 / OpenBLAS 0.3.29 results)."""
+    co = _load("ivclab/signal/color.py", "ref_color")
+    rng = np.random.default_rng(60)
+    c = {}
+    c["rgb_u8"] = rng.integers(0, 256, (48, 64, 3)).astype(np.uint8)
+    c["rgb_u8_ycc"] = co.rgb2ycbcr(c["rgb_u8"])
+    c["rgb_u8_gray"] = co.rgb2gray(c["rgb_u8"])
+    c["rgb_f64"] = rng.normal(128, 60, (40, 32, 3))
+    c["rgb_f64_ycc"] = co.rgb2ycbcr(c["rgb_f64"])
+    c["rgb_f64_gray"] = co.rgb2gray(c["rgb_f64"])
+    c["rgb_f32"] = rng.normal(128, 60, (16, 24, 3)).astype(np.float32)
+    c["rgb_f32_ycc"] = co.rgb2ycbcr(c["rgb_f32"])
+    c["rgb_f32_gray"] = co.rgb2gray(c["rgb_f32"])
+    c["rgb_i16"] = rng.integers(-300, 300, (8, 8, 3)).astype(np.int16)
+    c["rgb_i16_ycc"] = co.rgb2ycbcr(c["rgb_i16"])
+    c["ycc_f64"] = rng.normal(128, 90, (40, 48, 3))             # includes values that clip
+    c["ycc_f64_rgb"] = co.ycbcr2rgb(c["ycc_f64"])
+    c["ycc_f32"] = rng.normal(128, 90, (16, 16, 3)).astype(np.float32)
+    c["ycc_f32_rgb"] = co.ycbcr2rgb(c["ycc_f32"])
+    c["ycc_u8"] = rng.integers(0, 256, (8, 16, 3)).astype(np.uint8)
+    c["ycc_u8_rgb"] = co.ycbcr2rgb(c["ycc_u8"])
+    c["ycc4_f64"] = rng.normal(128, 40, (8, 8, 4))              # a 4th channel is ignored
+    c["ycc4_f64_rgb"] = co.ycbcr2rgb(c["ycc4_f64"])
+    c["round_trip"] = co.ycbcr2rgb(co.rgb2ycbcr(c["rgb_u8"]))
+    np.savez_compressed(os.path.join(OUT, "color.npz"), **c)
 
 
 if __name__ == "__main__":

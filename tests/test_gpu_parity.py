@@ -634,3 +634,36 @@ def test_intra_symbols_device_and_4k():
     torch.cuda.synchronize()
     assert int(nsym.item()) == want.size
     assert np.array_equal(short.cpu().numpy(), want[:12345])
+
+
+# ------------------------------------------------------------------------- colour ------
+def test_color_golden_gpu(golden):
+    from ivclab_amd.signal.color import rgb2gray, rgb2ycbcr, ycbcr2rgb
+    c = golden("color")
+    for k in ("rgb_u8", "rgb_f64", "rgb_f32", "rgb_i16"):
+        assert_bits(rgb2ycbcr(c[k]), c[f"{k}_ycc"], k)
+    for k in ("rgb_u8", "rgb_f64", "rgb_f32"):
+        assert_bits(rgb2gray(c[k]), c[f"{k}_gray"], k)
+    for k in ("ycc_f64", "ycc_f32", "ycc_u8", "ycc4_f64"):
+        assert_bits(ycbcr2rgb(c[k]), c[f"{k}_rgb"], k)
+    assert_bits(ycbcr2rgb(rgb2ycbcr(c["rgb_u8"])), c["round_trip"], "round trip")
+
+
+def test_color_large_vs_oracle():
+    """1080p frames: the elementwise conversions against NumPy itself, rgb2ycbcr against the
+    exact k-order-FMA restatement on a pixel sample (NumPy's own matmul depends on the host
+    BLAS kernel; the fixtures pin it where they were made)."""
+    from ivclab_amd.signal.color import rgb2gray, rgb2ycbcr, ycbcr2rgb
+    rng = np.random.default_rng(1080)
+    img = rng.integers(0, 256, (1080, 1920, 3), dtype=np.uint8)
+    ycc = rgb2ycbcr(img)
+    idx = rng.integers(0, 1080 * 1920, 1500)
+    want = O.rgb2ycbcr_fma(img.reshape(-1, 3)[idx][:, None, :])[:, 0, :]
+    assert_bits(ycc.reshape(-1, 3)[idx], want, "rgb2ycbcr sample")
+    assert_bits(ycbcr2rgb(ycc), O.ycbcr2rgb(ycc), "ycbcr2rgb")
+    assert_bits(rgb2gray(img), O.rgb2gray(img), "rgb2gray")
+    f = rng.normal(100, 80, (64, 64, 3)).astype(np.float32)
+    assert_bits(ycbcr2rgb(f), O.ycbcr2rgb(f), "f32")
+    assert_bits(rgb2gray(f), O.rgb2gray(f), "f32 gray")
+    with pytest.raises(ValueError):
+        rgb2ycbcr(np.zeros((4, 4, 2)))

@@ -150,3 +150,22 @@ def test_zerorun_decode_errors_golden(golden, case):
         assert f"{type(ei.value).__name__}: {ei.value}" == exc
     else:
         assert bits_equal(O.zerorun_decode(sym, shape), z[f"err_{case}_out"])
+
+
+def test_color_golden(golden):
+    c = golden("color")
+    for k in ("rgb_u8", "rgb_f64", "rgb_f32", "rgb_i16"):
+        assert bits_equal(O.rgb2ycbcr(c[k]), c[f"{k}_ycc"]), k
+    for k in ("rgb_u8", "rgb_f64", "rgb_f32"):
+        assert bits_equal(O.rgb2gray(c[k]), c[f"{k}_gray"]), k
+    for k in ("ycc_f64", "ycc_f32", "ycc_u8", "ycc4_f64"):
+        assert bits_equal(O.ycbcr2rgb(c[k]), c[f"{k}_rgb"]), k
+
+
+def test_rgb2ycbcr_is_korder_fma(golden):
+    """The kernel's arithmetic (k-order fused multiply-adds, then the offset) reproduces the
+    reference's matmul on the fixtures — the claim ivc_color.hip rests on."""
+    c = golden("color")
+    for k in ("rgb_u8", "rgb_f64"):
+        x = c[k][:6, :8]
+        assert bits_equal(O.rgb2ycbcr_fma(x), c[f"{k}_ycc"][:6, :8]), k

@@ -18,6 +18,7 @@ mkdir -p "$ROOT/ab"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math \
   "$@" -o "$ROOT/ab/$NAME.so" "$SRC"/ivclab_amd/csrc/ivc_kernels.hip "$SRC"/ivclab_amd/csrc/ivc_motion.hip \
   $( [ -f "$SRC"/ivclab_amd/csrc/ivc_entropy.hip ] && echo "$SRC"/ivclab_amd/csrc/ivc_entropy.hip ) \
+  $( [ -f "$SRC"/ivclab_amd/csrc/ivc_color.hip ] && echo "$SRC"/ivclab_amd/csrc/ivc_color.hip ) \
   "$SRC"/ivclab_amd/csrc/ivc_capi.hip
 rm -rf "$SRC"
 echo "built ab/$NAME.so"
