@@ -227,6 +227,20 @@ int ivc_minmax_i32_dev(const int32_t* sym, int64_t n, int32_t* mm, void* stream)
 int ivc_zerorun_decode_dev(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
                            int32_t eob, int32_t* out, int64_t* err, void* stream);
 
+/* ---------------------------------------------------------------- Huffman (host) --- */
+/* HuffmanCoder (ivclab/entropy/huffman.py:5-61) on the host, where the north star keeps the
+ * serial bit-packing.  lengths: Huffman code lengths of n weights (all > 0; ties merge in
+ * index order).  Canonical codes; bits MSB-first in 32-bit words.  Tie-breaking differs
+ * from the reference's `constriction` trees (absent here): bitstreams are not pinned.      */
+int ivc_huffman_lengths(const double* probs, int32_t n, uint8_t* lengths);
+/* symbols in [lower_bound, lower_bound + nalpha); IVC_E_ARG for a symbol outside, or
+ * IVC_E_SHAPE (with *nbits set) when cap_words is too small.                              */
+int ivc_huffman_encode(const int32_t* sym, int64_t n, int32_t lower_bound,
+                       const uint8_t* lengths, int32_t nalpha, uint32_t* words,
+                       int64_t cap_words, int64_t* nbits);
+int ivc_huffman_decode(const uint32_t* words, int64_t nwords, int64_t count, int32_t lower_bound,
+                       const uint8_t* lengths, int32_t nalpha, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,7 +23,8 @@ import types
 from .quantization import PatchQuant  # noqa: F401
 from .signal import DiscreteCosineTransform  # noqa: F401
 from .utils import Patcher, ZigZag  # noqa: F401
-from .entropy import ZeroRunCoder  # noqa: F401
+from .entropy import HuffmanCoder, ZeroRunCoder  # noqa: F401
+from .image import IntraCodec  # noqa: F401
 from .video import MotionCompensator  # noqa: F401
 
 __version__ = "0.1.0"
@@ -41,6 +42,9 @@ _ALIASES = {
     "ivclab.video": "ivclab_amd.video",
     "ivclab.video.motion": "ivclab_amd.video.motion",
     "ivclab.entropy": "ivclab_amd.entropy",
+    "ivclab.entropy.huffman": "ivclab_amd.entropy.huffman",
+    "ivclab.image": "ivclab_amd.image",
+    "ivclab.image.intracodec": "ivclab_amd.image.intracodec",
     "ivclab.entropy.zerorun": "ivclab_amd.entropy.zerorun",
 }
 
@@ -58,5 +62,5 @@ def install_as_ivclab() -> None:
         parent, _, leaf = name.rpartition(".")
         setattr(sys.modules[parent], leaf, mod)
     for cls in (PatchQuant, DiscreteCosineTransform, Patcher, ZigZag, MotionCompensator,
-                ZeroRunCoder):
+                ZeroRunCoder, HuffmanCoder, IntraCodec):
         setattr(root, cls.__name__, cls)

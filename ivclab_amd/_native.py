@@ -62,6 +62,9 @@ _SIGS = {
     "ivc_histogram_i32": ([_P, _L, _ct.c_int32, _ct.c_int32, _P], _I),
     "ivc_histogram_i32_dev": ([_P, _L, _ct.c_int32, _ct.c_int32, _P, _P], _I),
     "ivc_histogram_i64": ([_P, _L, _L, _ct.c_int32, _P], _I),
+    "ivc_huffman_lengths": ([_P, _ct.c_int32, _P], _I),
+    "ivc_huffman_encode": ([_P, _L, _ct.c_int32, _P, _ct.c_int32, _P, _L, _P], _I),
+    "ivc_huffman_decode": ([_P, _L, _L, _ct.c_int32, _P, _ct.c_int32, _P], _I),
     "ivc_rgb2ycbcr": ([_P, _ct.c_int, _L, _P], _I),
     "ivc_rgb2ycbcr_dev": ([_P, _ct.c_int, _L, _P, _P], _I),
     "ivc_ycbcr2rgb": ([_P, _ct.c_int, _L, _L, _P], _I),

@@ -489,6 +489,36 @@ int ivc_histogram_i32(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, 
   return st.sync();
 }
 
+// ---------------------------------------------------------------- Huffman (host) ------
+int ivc_huffman_lengths(const double* probs, int32_t n, uint8_t* lengths) {
+  CHECK(n >= 0 && probs && lengths, IVC_E_ARG, "huffman: bad arguments");
+  for (int32_t i = 0; i < n; ++i)
+    CHECK(probs[i] > 0, IVC_E_ARG,
+          "Zero-probability symbols found in PMF. All symbols must have non-zero probability.");
+  CHECK(huffman_lengths(probs, n, lengths) == 0, IVC_E_ARG, "huffman: code longer than 64 bits");
+  return IVC_OK;
+}
+
+int ivc_huffman_encode(const int32_t* sym, int64_t n, int32_t lower_bound,
+                       const uint8_t* lengths, int32_t nalpha, uint32_t* words,
+                       int64_t cap_words, int64_t* nbits) {
+  CHECK(n >= 0 && nalpha > 0 && nbits, IVC_E_ARG, "huffman_encode: bad arguments");
+  const int rc = huffman_encode(sym, n, lower_bound, lengths, nalpha, words, cap_words, nbits);
+  CHECK(rc != -1, IVC_E_ARG, "huffman_encode: invalid code lengths");
+  CHECK(rc != -2, IVC_E_ARG, "Message contains symbols outside the trained range.");
+  CHECK(rc != -3, IVC_E_SHAPE, "huffman_encode: output buffer too small");
+  return IVC_OK;
+}
+
+int ivc_huffman_decode(const uint32_t* words, int64_t nwords, int64_t count, int32_t lower_bound,
+                       const uint8_t* lengths, int32_t nalpha, int32_t* out) {
+  CHECK(nwords >= 0 && count >= 0 && nalpha > 0, IVC_E_ARG, "huffman_decode: bad arguments");
+  const int rc = huffman_decode(words, nwords, count, lower_bound, lengths, nalpha, out);
+  CHECK(rc != -1, IVC_E_ARG, "huffman_decode: invalid code lengths");
+  CHECK(rc == 0, IVC_E_ARG, "huffman_decode: the bitstream ends before message_length symbols");
+  return IVC_OK;
+}
+
 // ---------------------------------------------------------------- colour --------------
 static size_t color_out_size(int dtype) { return dtype == IVC_F32 ? 4 : 8; }
 

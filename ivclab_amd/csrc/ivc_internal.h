@@ -55,6 +55,11 @@ hipError_t launch_rgb2ycbcr(const void* src, int dtype, int64_t npix, double* ds
 hipError_t launch_ycbcr2rgb(const void* src, int dtype, int64_t npix, int64_t cstride, void* dst,
                             hipStream_t s);
 hipError_t launch_rgb2gray(const void* src, int dtype, int64_t npix, int C, void* dst, hipStream_t s);
+int huffman_lengths(const double* w, int32_t n, uint8_t* len);
+int huffman_encode(const int32_t* sym, int64_t n, int32_t lo, const uint8_t* len, int32_t nalpha,
+                   uint32_t* words, int64_t cap, int64_t* nbits);
+int huffman_decode(const uint32_t* words, int64_t nwords, int64_t count, int32_t lo,
+                   const uint8_t* len, int32_t nalpha, int32_t* out);
 hipError_t launch_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm, hipStream_t s);
 hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected, int B,
                                  int32_t eob, int32_t* out, void* scratch, int64_t* err,

@@ -33,3 +33,46 @@ def entropy_bits(pmf):
     p = np.asarray(pmf, dtype=np.float64)
     p = p[p > 0]
     return float(-(p * np.log2(p)).sum())
+
+
+def stats_marg(image, pixel_range):
+    """entropy.py:6-29 — np.histogram(image.astype(float64).flatten(), bins=pixel_range)
+    / image.size — for integer images over unit-spaced integer edges (the symbol and pixel
+    statistics of the codec), counted by the GPU histogram kernel.  np.histogram drops values
+    outside [edges[0], edges[-1]] and closes the last bin; the kernel clamps, so two guard
+    bins on each side absorb the out-of-range values and the top edge value is folded into
+    the last bin."""
+    from .. import _native as N
+    a = np.asarray(image)
+    edges = np.asarray(pixel_range)
+    if not (np.issubdtype(a.dtype, np.integer) or a.dtype == np.bool_):
+        raise NotImplementedError("stats_marg: integer images only")
+    if edges.ndim != 1 or edges.size < 2 or not np.issubdtype(edges.dtype, np.integer) or \
+            np.any(np.diff(edges) != 1):
+        raise NotImplementedError("stats_marg: unit-spaced integer bin edges only")
+    lo, nb = int(edges[0]), edges.size - 1
+    x = np.ascontiguousarray(a.ravel())
+    hist = np.zeros(nb + 3, np.int64)                  # [< lo | lo .. lo+nb-1 | lo+nb | > lo+nb]
+    if x.dtype.itemsize <= 4 and x.dtype != np.uint32:
+        x32 = x.astype(np.int32, copy=False)
+        N.check(N.lib().ivc_histogram_i32(N.ptr(x32), x32.size, lo - 1, nb + 3, N.ptr(hist)),
+                "stats_marg")
+    else:
+        x64 = x.astype(np.int64, copy=False)
+        N.check(N.lib().ivc_histogram_i64(N.ptr(x64), x64.size, lo - 1, nb + 3, N.ptr(hist)),
+                "stats_marg")
+    counts = hist[1:nb + 1].copy()
+    counts[-1] += hist[nb + 1]
+    return counts / x.size
+
+
+def calc_entropy(pmf, eps=1e-8):
+    """entropy.py:36-51."""
+    nonzero_pmf = pmf[pmf > 0]
+    return -np.sum(nonzero_pmf * np.log2(nonzero_pmf))
+
+
+def min_code_length(target_pmf, common_pmf, eps=1e-8):
+    """entropy.py:53-71."""
+    common_pmf = common_pmf + eps
+    return -np.sum(target_pmf * np.log2(common_pmf))

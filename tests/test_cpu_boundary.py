@@ -153,3 +153,36 @@ def test_symbol_pmf_from_counts_matches_stats_marg():
     got = smooth_pmf(stats_marg_from_counts(counts))
     want = O.smooth_pmf(O.stats_marg(sym, np.arange(b0, b1)))
     assert got.dtype == want.dtype and got.tobytes() == want.tobytes()
+
+
+def test_huffman_host_coder():
+    """libivc's host Huffman coder (no device needed): the reference module's own example
+    (huffman.py:55-61: 29 bits, exact round trip), the reference's errors, optimality on a
+    large alphabet (bit count = sum of code lengths, within 1 bit/symbol of the entropy)."""
+    from ivclab_amd.entropy import HuffmanCoder
+    h = HuffmanCoder(lower_bound=0)
+    with pytest.raises(RuntimeError):
+        h.encode(np.array([0]))
+    probs = np.array([0.5, 0.25, 0.25], dtype=np.float32)
+    msg = np.array([0, 2, 1, 2, 1, 0, 2, 0, 1, 0, 0, 2, 2, 0, 1, 0, 0, 2, 0])
+    h.train(probs)
+    comp, bits = h.encode(msg)
+    assert bits == 29.0
+    assert np.array_equal(h.decode(comp, len(msg)), msg)
+    assert h.is_prefix_free()
+    with pytest.raises(ValueError, match="outside the trained range"):
+        h.encode(np.array([3]))
+    with pytest.raises(ValueError, match="Zero-probability"):
+        HuffmanCoder().train(np.array([0.5, 0.0, 0.5]))
+    rng = np.random.default_rng(5)
+    p = rng.random(4000) ** 4 + 1e-9
+    p /= p.sum()
+    h2 = HuffmanCoder(lower_bound=-1000)
+    h2.train(p)
+    m = rng.choice(np.arange(-1000, 3000), size=300000, p=p)
+    comp, bits = h2.encode(m)
+    assert np.array_equal(h2.decode(comp, m.size), m)
+    L = h2.encoder_codebook.astype(np.float64)
+    assert bits == L[m + 1000].sum()
+    H = -(p * np.log2(p)).sum()
+    assert H <= (p * L).sum() < H + 1

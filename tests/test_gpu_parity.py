@@ -667,3 +667,85 @@ def test_color_large_vs_oracle():
     assert_bits(rgb2gray(f), O.rgb2gray(f), "f32 gray")
     with pytest.raises(ValueError):
         rgb2ycbcr(np.zeros((4, 4, 2)))
+
+
+# ---------------------------------------------------------------------- IntraCodec -----
+def _chain_symbols(ycc, scale):
+    """Oracle: image2symbols (intracodec.py:66-81) from an already colour-converted image."""
+    if ycc.ndim == 2:
+        ycc = ycc[:, :, None]
+    H, W, _ = ycc.shape
+    ph, pw = (8 - H % 8) % 8, (8 - W % 8) % 8
+    if ph or pw:
+        ycc = np.pad(ycc, ((0, ph), (0, pw), (0, 0)), mode="edge")
+    q = O.quantize(O.dct_transform(O.patch(ycc)), scale)
+    return O.zerorun_encode(O.zigzag_flatten(q))
+
+
+def _chain_image(sym, shape, scale):
+    """Oracle: symbols2image (intracodec.py:93-146)."""
+    if len(shape) == 2:
+        (H, W), C, rgb = shape, 1, False
+    else:
+        (H, W, C), rgb = shape, True
+    dec = O.zerorun_decode(sym, (H // 8, W // 8, C))
+    rec = O.unpatch(O.dct_inverse(O.dequantize(O.zigzag_unflatten(dec), scale)))
+    rec = rec[:H, :W, :]
+    if C == 1:
+        return rec[:, :, 0] if rec.shape[2] == 1 else rec
+    return O.ycbcr2rgb(rec) if rgb else rec
+
+
+@pytest.mark.parametrize("case", ["gray_u8", "gray_u8_pad", "gray_f64", "rgb_u8", "ycc_u8"])
+def test_intracodec_symbols_and_image(golden, case):
+    from ivclab_amd.image import IntraCodec
+    rng = np.random.default_rng(len(case))
+    scale = 0.6
+    codec = IntraCodec(quantization_scale=scale)
+    if case == "rgb_u8":
+        c = golden("color")
+        img, ycc, rgb = c["rgb_u8"], c["rgb_u8_ycc"], True
+    else:
+        shape = {"gray_u8": (64, 80), "gray_u8_pad": (50, 70), "gray_f64": (48, 56),
+                 "ycc_u8": (40, 48, 3)}[case]
+        img = rng.integers(0, 256, shape).astype(np.float64 if case == "gray_f64" else np.uint8)
+        if case == "gray_f64":
+            img = img + rng.random(shape)
+        ycc, rgb = img, False
+    sym = codec.image2symbols(img, is_source_rgb=rgb)
+    assert_bits(sym, _chain_symbols(ycc, scale), "image2symbols")
+    if case != "gray_u8_pad":
+        out_shape = img.shape
+        assert_bits(codec.symbols2image(sym, out_shape), _chain_image(sym, out_shape, scale),
+                    "symbols2image")
+
+
+def test_intracodec_encode_decode_roundtrip():
+    """Huffman-coded round trip: the decoded image is symbols2image(image2symbols(img)) and
+    the bit count is the sum of the symbols' code lengths."""
+    from ivclab_amd.image import IntraCodec
+    rng = np.random.default_rng(11)
+    img = rng.integers(0, 256, (64, 96, 3)).astype(np.uint8)
+    img[:32] = 128
+    codec = IntraCodec(quantization_scale=1.0)
+    codec.train_huffman_from_image(img)
+    rec, bitstream, bitsize, bpp = codec.encode_decode(img, return_bpp=True)
+    sym = codec.image2symbols(img)
+    assert np.array_equal(rec, codec.symbols2image(sym, img.shape))
+    L = codec.huffman.encoder_codebook
+    assert bitsize == float(L[sym - codec.bounds[0]].astype(np.int64).sum())
+    assert bpp == bitsize / (64 * 96)
+    assert codec.huffman.is_prefix_free()
+    bs, _ = codec.intra_encode(img)
+    assert np.array_equal(codec.intra_decode(bs, img.shape), rec)
+
+
+def test_stats_marg_gpu_vs_oracle():
+    """stats_marg on the GPU histogram equals np.histogram's counts (dropped out-of-range
+    values, closed last bin) divided by the sample count."""
+    from ivclab_amd.entropy import stats_marg
+    rng = np.random.default_rng(21)
+    for dt in (np.uint8, np.int16, np.int32, np.int64):
+        x = rng.integers(-300 if dt != np.uint8 else 0, 256, (50, 60)).astype(dt)
+        for edges in (np.arange(256), np.arange(-20, 41), np.arange(10, 12)):
+            assert_bits(stats_marg(x, edges), O.stats_marg(x, edges), f"{dt} {edges[0]}")

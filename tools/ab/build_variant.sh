@@ -19,6 +19,7 @@ mkdir -p "$ROOT/ab"
   "$@" -o "$ROOT/ab/$NAME.so" "$SRC"/ivclab_amd/csrc/ivc_kernels.hip "$SRC"/ivclab_amd/csrc/ivc_motion.hip \
   $( [ -f "$SRC"/ivclab_amd/csrc/ivc_entropy.hip ] && echo "$SRC"/ivclab_amd/csrc/ivc_entropy.hip ) \
   $( [ -f "$SRC"/ivclab_amd/csrc/ivc_color.hip ] && echo "$SRC"/ivclab_amd/csrc/ivc_color.hip ) \
+  $( [ -f "$SRC"/ivclab_amd/csrc/ivc_huffman.hip ] && echo "$SRC"/ivclab_amd/csrc/ivc_huffman.hip ) \
   "$SRC"/ivclab_amd/csrc/ivc_capi.hip
 rm -rf "$SRC"
 echo "built ab/$NAME.so"
