@@ -1,15 +1,22 @@
 """Benchmark of the ivclab block-codec hot path on MI355X (contract: one JSON line on rank 0).
 
-Workload (BASELINE.json configs[2], the metric's "4K intra DCT+quant" half): a batch of 256
-synthetic 3840x2160 luma frames per GPU, resident in HBM, through the fused
-patch -> DCT-II -> quantise kernel (reference-equivalent output: [F,270,480,3,64] int32,
-the C = 1 -> 3-plane broadcast of patchquant.py:59).  One step = one pass over the batch.
-Multi-GPU: one process per GPU, frames sharded (each rank owns its own 256 frames, weak
-scaling); after the timed steps each rank histograms its symbols and the ranks exchange
-them with one all-gather (the global Huffman table's input).
+Headline (`value`, BASELINE.json configs[2], the metric's "4K intra DCT+quant" half): a batch
+of 256 synthetic 3840x2160 luma frames per GPU, resident in HBM, through the fused
+patch -> DCT-II -> quantise kernel (reference-equivalent output: [F,270,480,3,64] int32, the
+C = 1 -> 3-plane broadcast of patchquant.py:59).  One step = one pass over the batch.
+`roofline` prices that kernel against HBM (13 B/px algorithmic, HIP events on its stream;
+`traffic` from the committed PMC record), `cpu_baseline` times the reference's algorithm
+(oracle) on one host core, `cpu_baseline_multicore` on the box's cores.
 
-The metric's other half ("+-16 full-search ME", configs[3]: 1080p x 300 frames, ME +
-MC + residual DCT + quantise) is measured in the same run and reported under "inter".
+Also reported from the same run:
+  zerorun / image2symbols  ZeroRunCoder on the zig-zag output, and pixels -> symbols fused
+  exchange                 global Huffman-table input: alphabet bounds (all-reduce) and the
+                           symbol histogram (all-gather), as IntraCodec trains it
+  inter                    configs[3]: 1080p x 300, +-16 full-search ME + MC + residual DCT+quant
+  sharded                  configs[4]: 8K x 120 frames split across the ranks (strong scaling),
+                           ME + residual DCT+quant + one histogram all-gather per step
+Multi-GPU: one process per GPU (torch.distributed, RCCL); cfg3/cfg4 are weak-scaled (each
+rank owns its frames), cfg5 strong-scaled.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--no-inter] [--no-cpu]
 """
