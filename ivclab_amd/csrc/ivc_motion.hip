@@ -308,7 +308,11 @@ __global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restri
   constexpr int WR = 8 + 2 * SR;            // window rows
   constexpr int WIN = WR * NW;              // window dwords fetched per block
   constexpr int P = Cfg::PITCH;             // LDS row pitch (>= NW)
-  constexpr int WINL = WR * P;              // LDS dwords per block window
+  // rows a lane reads: dy0 + 0 .. dy0 + DYT + 6 for dy0 up to (NDR - 1) DYT; rows past the
+  // window (only for candidates dy >= N, masked at selection) read unwritten LDS instead of
+  // being tested and zeroed per row
+  constexpr int ROWS = WR > NDR * DYT + 7 ? WR : NDR * DYT + 7;
+  constexpr int WINL = ROWS * P;            // LDS dwords per block window
   constexpr int PW = (BPW * WIN + 63) / 64; // window dwords staged per lane
   constexpr int CUR = BPW * 16;             // cur dwords per group (<= 64)
   constexpr int STAGE = BPW * WINL + CUR;
@@ -408,10 +412,8 @@ __global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restri
       // row words are read one row ahead of their use (the fence below would otherwise
       // expose the LDS latency once per row)
       auto row_words = [&](int row, uint32_t& a0, uint32_t& a1, uint32_t& a2) {
-        const bool in = row < WR;
-        const uint32_t* p = win + (in ? row : 0) * P + g;
+        const uint32_t* p = win + row * P + g;
         a0 = p[0]; a1 = p[1]; a2 = p[2];
-        if (!in) { a0 = 0u; a1 = 0u; a2 = 0u; }
       };
       uint32_t w0, w1, w2;
       row_words(dy0, w0, w1, w2);
