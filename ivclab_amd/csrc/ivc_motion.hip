@@ -242,9 +242,15 @@ __global__ __launch_bounds__(256) void me_s2_kernel(const uint8_t* __restrict__ 
       for (int k = 0; k < 8; ++k) {
         const int yy = y + k;
         if (yy < y1) {
+          if (nvalid == 4) {
+            // 16-byte aligned: x and W are multiples of 4 and 8
+            *reinterpret_cast<int4*>(out + (int64_t)yy * W) =
+                make_int4((int)acc[0], (int)acc[1], (int)acc[2], (int)acc[3]);
+          } else {
 #pragma unroll
-          for (int s = 0; s < 4; ++s)
-            if (s < nvalid) out[(int64_t)yy * W + s] = (int32_t)acc[s];
+            for (int s = 0; s < 4; ++s)
+              if (s < nvalid) out[(int64_t)yy * W + s] = (int32_t)acc[s];
+          }
           if (yy + 1 < y1) {                       // slide: drop row yy, add row yy + 8
             uint32_t hn[4];
             s2_hrow(rs, (yy + 8) * W + x, hn);
