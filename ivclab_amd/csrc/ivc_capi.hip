@@ -604,8 +604,8 @@ int ivc_zerorun_encode_dev(const int32_t* src, int64_t nblk, int32_t row_stride,
   int32_t* counts = nullptr;
   int64_t* agg = nullptr;
   if (nblk > 0) {
-    hipError_t e = hipMallocAsync((void**)&counts, (size_t)nblk * 4, s);
-    if (e == hipSuccess) e = hipMallocAsync((void**)&agg, (size_t)scan_scratch_elems(nblk) * 8, s);
+    hipError_t e = scratch_alloc((void**)&counts, (size_t)nblk * 4, s);
+    if (e == hipSuccess) e = scratch_alloc((void**)&agg, (size_t)scan_scratch_elems(nblk) * 8, s);
     if (e != hipSuccess) return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
   }
   int rc = dev_launch(launch_zerorun_offsets(src, nblk, row_stride, block_size, counts, agg, offsets, s),
@@ -659,7 +659,7 @@ int ivc_zerorun_decode_dev(const int32_t* sym, int64_t nsym, int64_t nblk, int32
   TRY(check_zr_dec(nsym, nblk, block_size));
   hipStream_t s = (hipStream_t)stream;
   void* scratch = nullptr;
-  hipError_t e = hipMallocAsync(&scratch, (size_t)zr_decode_scratch_bytes(nsym), s);
+  hipError_t e = scratch_alloc(&scratch, (size_t)zr_decode_scratch_bytes(nsym), s);
   if (e != hipSuccess) return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
   const int rc = dev_launch(launch_zerorun_decode(sym, nsym, nblk, block_size, eob, out, scratch, err, s),
                             "zerorun_decode");

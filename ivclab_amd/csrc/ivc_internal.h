@@ -39,6 +39,7 @@ hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int6
 hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, int unzigzag,
                                double* out, hipStream_t s);
 unsigned resident_grid_ptr(const void* kernel, int64_t work_groups_needed);
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 // zero-run coding (ivc_entropy.hip)
 int64_t scan_scratch_elems(int64_t n);
 hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* agg, int64_t* off,

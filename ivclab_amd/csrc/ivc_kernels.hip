@@ -847,6 +847,25 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
 }
 
 
+// Library scratch is stream-ordered (hipMallocAsync on the caller's stream).  The device's
+// default memory pool is told once to keep freed blocks, so repeated calls reuse memory
+// instead of mapping and unmapping gigabytes per call.
+static std::once_flag g_pool_once[64];
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev >= 0 && dev < 64)
+    std::call_once(g_pool_once[dev], [dev] {
+      hipMemPool_t pool;
+      if (hipDeviceGetDefaultMemPool(&pool, dev) == hipSuccess) {
+        uint64_t keep = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+      }
+    });
+  return hipMallocAsync(p, bytes ? bytes : 16, s);
+}
+
 static std::mutex g_occ_mu;
 static std::unordered_map<const void*, int> g_occ;
 
@@ -1005,9 +1024,9 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
   int32_t* counts = nullptr;
   int64_t* agg = nullptr;
   int64_t* off = nullptr;
-  hipError_t e = hipMallocAsync((void**)&counts, (size_t)ngroups * 4, s);
-  if (e == hipSuccess) e = hipMallocAsync((void**)&agg, (size_t)scan_scratch_elems(ngroups) * 8, s);
-  if (e == hipSuccess) e = hipMallocAsync((void**)&off, (size_t)(ngroups + 1) * 8, s);
+  hipError_t e = scratch_alloc((void**)&counts, (size_t)ngroups * 4, s);
+  if (e == hipSuccess) e = scratch_alloc((void**)&agg, (size_t)scan_scratch_elems(ngroups) * 8, s);
+  if (e == hipSuccess) e = scratch_alloc((void**)&off, (size_t)(ngroups + 1) * 8, s);
   if (e == hipSuccess) {
     a.zr_counts = counts;
     a.zr_off = off;

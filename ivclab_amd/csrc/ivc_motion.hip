@@ -18,25 +18,12 @@
 
 namespace ivc {
 
-// per-device scratch for the S2 pre-pass (grown on demand, never shrunk; one stream at a
-// time per device is assumed for this buffer, like the host-staging scratch in the C-ABI)
-static int32_t* g_s2[64] = {};
-static size_t g_s2_cap[64] = {};
-static int32_t* me_s2_scratch(int64_t elems, hipStream_t s) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  const size_t bytes = (size_t)elems * 4;
-  if (g_s2_cap[dev] < bytes) {
-    if (g_s2[dev]) {
-      (void)hipStreamSynchronize(s);
-      (void)hipFree(g_s2[dev]);
-    }
-    g_s2[dev] = nullptr;
-    g_s2_cap[dev] = 0;
-    if (hipMalloc(&g_s2[dev], bytes) != hipSuccess) return nullptr;
-    g_s2_cap[dev] = bytes;
-  }
-  return g_s2[dev];
+// S2 scratch: stream-ordered (scratch_alloc / hipFreeAsync on the launch stream), so
+// concurrent streams never share it.
+static int32_t* me_s2_alloc(int64_t elems, hipStream_t s) {
+  void* p = nullptr;
+  if (scratch_alloc(&p, (size_t)elems * 4, s) != hipSuccess) return nullptr;
+  return (int32_t*)p;
 }
 
 static int g_cus = 0;
@@ -510,7 +497,7 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
     if (dtype != IVC_U8) return hipErrorInvalidValue;
     if (sr == 4 || sr == 8 || sr == 16) {
       // S2 scratch: one int32 per pixel of the reference frames (library-owned, grown once)
-      int32_t* s2 = me_s2_scratch(nframes * H * W, s);
+      int32_t* s2 = me_s2_alloc(nframes * H * W, s);
       if (!s2) return hipErrorOutOfMemory;
       me_s2_kernel<<<me_grid(nframes * ((W - 8) / 4 + 1) * ((H - 8) / S2Y + 1), 256, 8), 256, 0, s>>>(
           (const uint8_t*)ref, nframes, h, w, s2);
@@ -528,6 +515,7 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
         default: ME_FAST(16, 1); break;
       }
 #undef ME_FAST
+      (void)hipFreeAsync(s2, s);
       return hipGetLastError();
     }
     switch (sr) {
