@@ -256,7 +256,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=6)
     ap.add_argument("--frames", type=int, default=256)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--width", type=int, default=3840)
@@ -293,6 +293,8 @@ def main():
         D.intra_encode(frames, table, out, zigzag=args.zigzag)
 
     wall, kern_ms = timed(dist, step, args.steps, args.warmup)
+    from ivclab_amd import _native as N
+    pace_rate, pace_late = N.lib().ivc_store_pace(), N.lib().ivc_store_pace_late()
 
     # write-stream ceiling for this buffer: the same 12 B/px of int32 output written by
     # torch's vectorised fill kernel (no reads) — what the store side alone can reach
@@ -362,7 +364,11 @@ def main():
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": "fused_encode_kernel<u8,f64,C=1>",
                      "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": algo_bytes,
-                     "write_ceiling_GBs": round(fill_gbs, 1)},
+                     "write_ceiling_GBs": round(fill_gbs, 1),
+                     "store_pace": {"total_GBs": round(pace_rate, 1),
+                                    "late_fraction": round(pace_late, 4),
+                                    "note": "clock-paced address-ordered store sweep, rate "
+                                            "adapted per launch (DESIGN.md §5)"}},
         "zerorun": {"blocks_per_gpu": nblk, "symbols_per_gpu": nsym,
                     "ms": round(zms, 3), "Mblocks_per_s": round(nblk / zms / 1e3, 1),
                     "note": "ZeroRunCoder.encode of the zig-zag output (count, scan, emit kernels)",

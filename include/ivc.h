@@ -58,6 +58,18 @@ int ivc_set_device(int device);
 int ivc_device_ok(void);
 /* release the library's cached scratch buffers on the current device */
 int ivc_release_scratch(void);
+/* Store pacing of the fused coefficient encoders (ivc_intra_encode*, ivc_inter_encode*):
+ * persistent waves release their output stores on the chip-wide clock so that the stores
+ * in flight sweep the output in address order.  The rate is the total HBM
+ * rate (input + output GB/s) the sweep is timed for; it adapts per device from each launch's
+ * count of late slots.  ivc_set_store_pace sets the starting rate (0 turns pacing off;
+ * default: the IVC_PACE_GBPS environment variable, else the library's built-in rate);
+ * ivc_store_pace returns the current device's rate, ivc_store_pace_late the late fraction
+ * of the last measured launch (-1 if none).  Timing only: outputs are identical with and
+ * without pacing.  No reference counterpart.                                             */
+int ivc_set_store_pace(double total_gbps);
+double ivc_store_pace(void);
+double ivc_store_pace_late(void);
 
 /* ---------------------------------------------------------------- DCT -------------- */
 /* 2-D DCT-II (inverse=0) / DCT-III (inverse=1) of nblk contiguous 8x8 blocks, applied along

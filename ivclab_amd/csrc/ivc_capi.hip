@@ -195,6 +195,16 @@ int ivc_device_ok(void) {
   return strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
+int ivc_set_store_pace(double total_gbps) {
+  if (!(total_gbps >= 0)) return fail(IVC_E_ARG, "ivc_set_store_pace: rate must be >= 0");
+  set_store_pace_gbps(total_gbps);
+  return IVC_OK;
+}
+
+double ivc_store_pace(void) { return store_pace_gbps(); }
+
+double ivc_store_pace_late(void) { return store_pace_late_fraction(); }
+
 int ivc_release_scratch(void) {
   int dev = 0;
   TRY(current_device(&dev));

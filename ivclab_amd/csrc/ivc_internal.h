@@ -38,6 +38,10 @@ hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int6
                                hipStream_t s);
 hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, int unzigzag,
                                double* out, hipStream_t s);
+// store pacing of the fused coefficient kernels (ivc_kernels.hip): target total HBM GB/s, 0 = off
+double store_pace_gbps();
+double store_pace_late_fraction();
+void set_store_pace_gbps(double gbps);
 unsigned resident_grid_ptr(const void* kernel, int64_t work_groups_needed);
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 // zero-run coding (ivc_entropy.hip)

@@ -12,6 +12,8 @@
 // through LDS -> column pass (thread now owns column r) -> results staged in LDS -> the
 // workgroup writes its contiguous output span with 16-byte stores.  HBM traffic per unit
 // is one read of the input and one write of the output.
+#include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
@@ -336,6 +338,11 @@ struct FusedArgs {
   int32_t* zr_out;
   int64_t zr_cap;
   int32_t zr_eob;
+  // store pacing (OUT_COEFS): slot s of wave w (of W) stores no earlier than
+  // (*pace_t0 + (s * pace_d + w * pace_d / W) / 256) on the 100 MHz s_memrealtime clock;
+  // pace_d = 0: unpaced
+  uint64_t* pace_t0;     // pace block (pace_stamp_kernel): start time, late-slot counters
+  uint32_t pace_d;       // 1/256 clock ticks per slot
 #ifdef IVC_ABLATION
   int ablate;            // diagnostic builds only (tools/ablate): bit mask of skipped phases
 #endif
@@ -359,6 +366,12 @@ struct FusedArgs {
 #ifndef IVC_FUSED_GRID
 #define IVC_FUSED_GRID 0
 #endif
+#ifndef IVC_PACE_DEFAULT_GBPS
+#define IVC_PACE_DEFAULT_GBPS 5800.0   // starting total HBM GB/s of the paced store sweep
+#endif
+#ifndef IVC_PREFETCH
+#define IVC_PREFETCH 2   // load tiles in flight per wave (small tiles)
+#endif
 #ifndef IVC_WIDE_NG
 #define IVC_WIDE_NG 2    // u8 luma: 8 rows x 128 bytes per wave load (whole cache lines)
 #endif
@@ -379,6 +392,36 @@ struct WaveLds {
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+
+// Store pacing.  A persistent grid whose waves store their groups as soon as they are
+// computed scatters the concurrently written output over every wave's current group plus the
+// waves' accumulated drift (tens of MiB), and HBM writes lose ~10-20% against an address-
+// ordered sweep (tools/ubench/store_pattern4.hip, _6.hip).  Paced, wave w of W releases its
+// slot-s store at t0 + s*D + w*D/W on the chip-wide constant clock, so the stores in flight at
+// any instant are a few adjacent groups that sweep the buffer in address order, and no wave
+// drifts.  A late wave stores at once; pacing never changes what is stored, only when.
+// The rate the device sustains varies from board to board, and a schedule faster than it is
+// worse than none (early waves idle while late ones store out of order), so every launch
+// counts its late slots (more than a slot behind) and the host adapts the rate between
+// launches (setup_pacing).
+// Returns 1 if the slot was more than `slack` (1/256 ticks) late.
+__device__ __forceinline__ uint32_t pace_until(uint64_t t256, uint32_t slack) {
+  uint64_t now = __builtin_amdgcn_s_memrealtime();
+  const uint32_t late = (now << 8) > t256 + slack ? 1u : 0u;
+  while ((now << 8) < t256) {
+    __builtin_amdgcn_s_sleep(1);
+    now = __builtin_amdgcn_s_memrealtime();
+  }
+  return late;
+}
+
+// pace block: [0] start time (ticks), [1..8] late-slot counters (sharded: one atomic word
+// saturates near 90 updates/us)
+constexpr int PACE_SHARDS = 8;
+__global__ void pace_stamp_kernel(uint64_t* blk, uint32_t lead) {
+  blk[0] = __builtin_amdgcn_s_memrealtime() + lead;
+  for (int i = 1; i <= PACE_SHARDS; ++i) blk[i] = 0;
 }
 
 // A group = 8 horizontally adjacent blocks of one block row (one wave-step of compute and
@@ -800,50 +843,115 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
   const uint32_t nwaves = gridDim.x * 4u;
   uint32_t lt = blockIdx.x * 4u + wave;
 
-  // Software pipeline per wave.  Group (lt, g) first issues the stores of the previous group
-  // (staged in LDS); group 0 then issues the prefetch of load tile lt + nwaves; then the
-  // group is transformed.  The prologue issues the same number of (range-dropped) stores, so
-  // every path into a wait for tile lt's rows has the same ops behind that load and the
-  // compiler's vmcnt wait never includes the stores.  Ragged / non-existent groups go
-  // through zero-range descriptors instead of branches.
-  TileRaw<TI, C, NG> raw;
-  if constexpr (SRC == SRC_IMAGE) {
-    load_tile<TI, C, NG>(a, lt, lt < nlt, lane, raw);
+  // pacing clock of this wave's slots (slot = groups stored so far), in 1/256 ticks
+  uint64_t pace_next = 0;
+  if (OUTM == OUT_COEFS && a.pace_d)
+    pace_next = (*a.pace_t0 << 8) + (uint64_t)a.pace_d * (blockIdx.x * 4u + wave) / nwaves;
+  uint32_t nlate = 0;
+  auto store_prev = [&](uint32_t plt, int pg, bool have_prev) {
     if constexpr (OUTM == OUT_COEFS) {
-#pragma unroll
-      for (int g = 1; g < NG; ++g) store_group<NG, C, DUP>(a, os, lane, 0u, 0, false);
+      if (a.pace_d && have_prev) {
+        nlate += pace_until(pace_next, a.pace_d);
+        pace_next += a.pace_d;
+      }
+      store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
     }
-  }
+  };
   uint32_t plt = 0;
   int pg = 0;
   bool have_prev = false;
-  for (; lt < nlt; lt += nwaves) {
-    TileRaw<TI, C, NG> nraw;
+
+  constexpr int PF = (SRC == SRC_IMAGE && TileRaw<TI, C, NG>::NW <= 8) ? IVC_PREFETCH : 1;
+  if constexpr (PF > 1) {
+    // Software pipeline per wave in rounds of PF load tiles (nwaves apart).  At the start of
+    // a round the wave issues the loads of the whole next round at once, so the chip's read
+    // stream arrives in bursts between long runs of stores instead of an even 1:12 mix with
+    // them (HBM read/write turnarounds: tools/ubench/store_pattern8.hip); the next round's
+    // tiles land in a second register ring that becomes the current one at the round's end
+    // (its wait covers loads a whole round old).  Every group first issues the stores of the
+    // previous group (staged in LDS).  Ragged and past-the-end tiles go through zero-range
+    // descriptors instead of branches.
+    TileRaw<TI, C, NG> ring[PF];
 #pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      if constexpr (OUTM == OUT_COEFS)
-        store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
-      RowReg<TI, C, SRC> v;
-      if constexpr (SRC == SRC_IMAGE) {
-        if (g == 0) {
-          const uint32_t nt = lt + nwaves;
-          load_tile<TI, C, NG>(a, nt, nt < nlt && !IVC_SKIP(a, 32), lane, nraw);
-        }
-        group_row<TI, C, NG>(raw, g, lane, v);
-      } else {
-        gather_inter(a, lt, b, r, v);
-      }
-      encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
-      if constexpr (OUTM != OUT_COEFS)
-        zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, lt, g).nb, (int64_t)lt * NG + g);
-      plt = lt;
-      pg = g;
-      have_prev = true;
+    for (int p = 0; p < PF; ++p) {
+      const uint32_t t0 = lt + p * nwaves;
+      load_tile<TI, C, NG>(a, t0, t0 < nlt && !IVC_SKIP(a, 32), lane, ring[p]);
     }
-    if constexpr (SRC == SRC_IMAGE) raw = nraw;
+    for (; lt < nlt; lt += PF * nwaves) {
+      TileRaw<TI, C, NG> nxt[PF];
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const uint32_t nt = lt + (PF + p) * nwaves;
+        load_tile<TI, C, NG>(a, nt, nt < nlt && !IVC_SKIP(a, 32), lane, nxt[p]);
+      }
+#pragma unroll
+      for (int p = 0; p < PF; ++p) {
+        const uint32_t tp = lt + p * nwaves;
+        const bool ex = tp < nlt;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+          store_prev(plt, pg, have_prev);
+          RowReg<TI, C, SRC> v;
+          group_row<TI, C, NG>(ring[p], g, lane, v);
+          encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+          if constexpr (OUTM != OUT_COEFS) {
+            if (ex) zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, tp, g).nb, (int64_t)tp * NG + g);
+          }
+          plt = tp;
+          pg = g;
+          have_prev = ex;
+        }
+      }
+#pragma unroll
+      for (int p = 0; p < PF; ++p) ring[p] = nxt[p];
+    }
+  } else {
+    // Software pipeline per wave, one tile ahead.  Group (lt, g) first issues the stores of
+    // the previous group (staged in LDS); group 0 then issues the prefetch of load tile
+    // lt + nwaves; then the group is transformed.  The prologue issues the same number of
+    // (range-dropped) stores, so every path into a wait for tile lt's rows has the same ops
+    // behind that load and the compiler's vmcnt wait never includes the stores.
+    TileRaw<TI, C, NG> raw;
+    if constexpr (SRC == SRC_IMAGE) {
+      load_tile<TI, C, NG>(a, lt, lt < nlt, lane, raw);
+      if constexpr (OUTM == OUT_COEFS) {
+#pragma unroll
+        for (int g = 1; g < NG; ++g) store_group<NG, C, DUP>(a, os, lane, 0u, 0, false);
+      }
+    }
+    for (; lt < nlt; lt += nwaves) {
+      TileRaw<TI, C, NG> nraw;
+#pragma unroll
+      for (int g = 0; g < NG; ++g) {
+        store_prev(plt, pg, have_prev);
+        RowReg<TI, C, SRC> v;
+        if constexpr (SRC == SRC_IMAGE) {
+          if (g == 0) {
+            const uint32_t nt = lt + nwaves;
+            load_tile<TI, C, NG>(a, nt, nt < nlt && !IVC_SKIP(a, 32), lane, nraw);
+          }
+          group_row<TI, C, NG>(raw, g, lane, v);
+        } else {
+          gather_inter(a, lt, b, r, v);
+        }
+        encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+        if constexpr (OUTM != OUT_COEFS)
+          zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, lt, g).nb, (int64_t)lt * NG + g);
+        plt = lt;
+        pg = g;
+        have_prev = true;
+      }
+      if constexpr (SRC == SRC_IMAGE) raw = nraw;
+    }
   }
-  if constexpr (OUTM == OUT_COEFS)
+  if constexpr (OUTM == OUT_COEFS) {
+    if (a.pace_d && have_prev) nlate += pace_until(pace_next, a.pace_d);
     store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+    if (nlate && lane == 0)
+      __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.pace_t0) + 1 +
+                                 blockIdx.x % PACE_SHARDS,
+                             (unsigned long long)nlate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 
@@ -895,6 +1003,131 @@ static unsigned resident_grid(K kernel, int64_t work_groups_needed) {
   return resident_grid_ptr(reinterpret_cast<const void*>(kernel), work_groups_needed);
 }
 
+// Store pacing of the coefficient-writing fused kernels (see pace_until).  The rate is the
+// total HBM rate (input + output bytes) the paced sweep is timed for.  It adapts per device
+// between launches: a launch whose late slots exceed PACE_LATE_HI of its slots lowers it by
+// 2% and marks it too fast; otherwise it creeps up by 0.5%, never past 99% of the lowest rate
+// seen too fast (a mark that itself rises 0.2% per good launch).  A launch's late count is read back without blocking (a pinned host copy
+// behind an event) when a later launch is set up.  IVC_PACE_GBPS / ivc_set_store_pace set the
+// starting rate (0 disables pacing).
+static std::mutex g_pace_mu;
+static double g_pace_start = -1.0;
+// late-slot fractions are bimodal: < 1% below the device's rate, 20-50% once over it
+constexpr double PACE_LATE_HI = 0.05, PACE_MAX_GBPS = 7600.0;
+
+struct PaceState {
+  uint64_t* blk = nullptr;        // device pace block
+  uint64_t* host = nullptr;       // pinned copy of the late counters
+  hipEvent_t ev = nullptr;
+  bool pending = false;           // a measured launch's counters are on their way
+  bool arm = false;               // the launch being set up is the one to measure
+  double slots = 0;               // slots of the measured launch
+  double rate = 0, too_fast = 1e30, last_late = -1;
+};
+// per device and per encoder (0: image source, 1: inter residual source)
+static PaceState g_pace[64][2];
+
+static double pace_start_rate() {
+  if (g_pace_start < 0) {
+    const char* e = getenv("IVC_PACE_GBPS");
+    g_pace_start = e ? atof(e) : IVC_PACE_DEFAULT_GBPS;
+    if (!(g_pace_start >= 0)) g_pace_start = 0;
+  }
+  return g_pace_start;
+}
+
+double store_pace_gbps() {
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && g_pace[dev][0].blk)
+    return g_pace[dev][0].rate;
+  return pace_start_rate();
+}
+
+double store_pace_late_fraction() {
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
+  return g_pace[dev][0].last_late;
+}
+
+void set_store_pace_gbps(double gbps) {
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  g_pace_start = gbps > 0 ? gbps : 0.0;
+  for (auto& d : g_pace)
+    for (auto& p : d) {
+      p.rate = g_pace_start;
+      p.too_fast = 1e30;
+    }
+}
+
+// Turns pacing on for a launch of `nwaves` persistent waves that store `slots` groups each
+// (of `group_bytes` input + output bytes): a one-lane kernel on the same stream stamps the
+// start time (the clock a few microseconds ahead, covering the launch gap) and clears the
+// late counters.  Concurrent launches on other streams may overwrite the device's pace block
+// between a stamp and its kernel; that only shifts a schedule by a launch gap or blurs one
+// launch's late count.
+static void setup_pacing(FusedArgs& a, int kind, int64_t nwaves, int64_t slots,
+                         double group_bytes, hipStream_t s) {
+  if (slots < 8) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  PaceState& P = g_pace[dev][kind];
+  if (!P.blk) {
+    if (pace_start_rate() <= 0) return;
+    if (hipMalloc((void**)&P.blk, 8 * (1 + PACE_SHARDS)) != hipSuccess ||
+        hipHostMalloc((void**)&P.host, 8 * PACE_SHARDS, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreateWithFlags(&P.ev, hipEventDisableTiming) != hipSuccess) {
+      (void)hipGetLastError();
+      P.blk = nullptr;
+      return;
+    }
+    P.rate = pace_start_rate();
+  }
+  if (P.pending && hipEventQuery(P.ev) == hipSuccess) {
+    uint64_t late = 0;
+    for (int i = 0; i < PACE_SHARDS; ++i) late += P.host[i];
+    P.last_late = (double)late / P.slots;
+    if (P.last_late > PACE_LATE_HI) {
+      P.too_fast = std::min(P.too_fast, P.rate);
+      P.rate *= 0.98;
+    } else {
+      P.too_fast *= 1.002;       // forget slowly: a transient must not cap the rate for good
+      const double cap = std::min(PACE_MAX_GBPS, 0.99 * P.too_fast);
+      P.rate = std::max(std::min(P.rate * 1.005, cap), P.rate);
+    }
+    P.pending = false;
+  }
+  (void)hipGetLastError();
+  if (P.rate <= 0) return;
+  // ticks (10 ns) per slot: the whole grid's slot bytes at the target rate
+  const double d256 = (double)nwaves * group_bytes / (P.rate * 1e9) * 1e8 * 256.0;
+  if (!(d256 >= 1.0) || d256 > 4.0e9) return;
+  pace_stamp_kernel<<<1, 1, 0, s>>>(P.blk, 300u);
+  a.pace_t0 = P.blk;
+  a.pace_d = (uint32_t)d256;
+  if (!P.pending) {
+    P.slots = (double)nwaves * (double)slots;
+    P.pending = P.arm = true;
+  }
+}
+
+// After a paced launch: queue the copy-back of its late counters if it is the measured one.
+static void finish_pacing(int kind, hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  PaceState& P = g_pace[dev][kind];
+  if (!P.arm) return;
+  P.arm = false;
+  if (hipMemcpyAsync(P.host, P.blk + 1, 8 * PACE_SHARDS, hipMemcpyDeviceToHost, s) != hipSuccess ||
+      hipEventRecord(P.ev, s) != hipSuccess) {
+    (void)hipGetLastError();
+    P.pending = false;
+  }
+}
+
 // NG: groups of 8 blocks per wave load (wide, whole-cache-line row loads for u8 luma)
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CM,
           int NGW = IVC_WIDE_NG>
@@ -915,13 +1148,18 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
       return (unsigned)(g < 1 ? 1 : g);
     }
   };
-  if (C == 1 && a.dup12) {
-    auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, C == 1>;
-    k<<<grid(k), 256, 0, s>>>(a, t);
-  } else {
-    auto k = fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, false>;
-    k<<<grid(k), 256, 0, s>>>(a, t);
-  }
+  // input + output bytes of one group (8 blocks)
+  const double gbytes = 8.0 * (SRC == SRC_INTER ? 64.0 * 2 + 8.0 + 768.0
+                                                : 64.0 * C * sizeof(TI) + 768.0);
+  auto go = [&](auto k) {
+    const unsigned g = grid(k);
+    const int64_t nw = 4 * (int64_t)g;
+    setup_pacing(a, SRC, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
+    k<<<g, 256, 0, s>>>(a, t);
+    if (a.pace_d) finish_pacing(SRC, s);
+  };
+  if (C == 1 && a.dup12) go(fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, C == 1>);
+  else go(fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, false>);
 }
 
 // The FAST quotient check needs |quotient| < 2^20.  Integer pixels
@@ -959,6 +1197,8 @@ static FusedArgs make_fused_args(const void* img, const int64_t* mv, int32_t* ou
   a.zr_out = nullptr;
   a.zr_cap = 0;
   a.zr_eob = 0;
+  a.pace_t0 = nullptr;
+  a.pace_d = 0;
   a.dup12 = 1;
   for (int i = 0; i < 64; ++i)
     if (t.q[64 + i] != t.q[128 + i]) a.dup12 = 0;

@@ -340,6 +340,42 @@ def test_intra_encode_4k_full_frame():
     assert_bits(out[0], want, "4K intra")
 
 
+def test_store_pacing_changes_timing_only():
+    """Paced launches (8 4K frames: every wave stores >= 8 slots, so the clock schedule is
+    live) give the same bytes as unpaced ones at any rate — far too fast (every slot late),
+    adaptive default, far too slow (every wave waits) — and the pace API reports the rate and
+    the late fraction it adapts from.  Frame 0 is checked against the oracle."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    N, L = _native()
+    rng = np.random.default_rng(88)
+    F, H, W = 8, 2160, 3840
+    img = rng.integers(0, 256, (F, H, W, 1), dtype=np.uint8)
+    img[:, 500:700] = 31                                        # flat rows: DC ties
+    x = torch.from_numpy(img).cuda()
+    table = PatchQuant(1.0).get_quantization_table()
+    outs = {}
+    start = L.ivc_store_pace()
+    try:
+        for rate in (0.0, 1e6, 5800.0, 600.0):
+            N.check(L.ivc_set_store_pace(rate))
+            assert L.ivc_store_pace() == rate
+            o = torch.full((F, H // 8, W // 8, 3, 64), -7, dtype=torch.int32, device="cuda")
+            for _ in range(3):                                  # adaptive steps in between
+                D.intra_encode(x, table, o)
+            torch.cuda.synchronize()
+            outs[rate] = o.cpu().numpy()
+            late = L.ivc_store_pace_late()
+            assert late == -1.0 or 0.0 <= late <= 1.0
+        assert L.ivc_set_store_pace(-1.0) == N.E_ARG
+    finally:
+        N.check(L.ivc_set_store_pace(start))
+    for rate, o in outs.items():
+        assert_bits(o, outs[0.0], f"paced at {rate} GB/s")
+    want = O.intra_encode(img[0], 1.0).reshape(H // 8, W // 8, 3, 64)
+    assert_bits(outs[5800.0][0], want, "paced 4K frame 0")
+
+
 def test_histogram_vs_oracle():
     N, L = _native()
     rng = np.random.default_rng(1)

@@ -15,7 +15,8 @@ ROOT = os.path.dirname(os.path.dirname(HERE))
 VARIANT = os.environ.get("ABL_DEFS", "")   # e.g. "-DIVC_STORE_AUX=2 -DIVC_LOAD_AUX=2"
 so = "/tmp/ivc_ablate%s.so" % abs(hash(VARIANT))
 subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-                "-ffp-contract=off", *VARIANT.split(), "-o", so, os.path.join(HERE, "ablate.hip")], check=True)
+                "-ffp-contract=off", *VARIANT.split(), "-o", so, os.path.join(HERE, "ablate.hip"),
+                os.path.join(ROOT, "ivclab_amd", "csrc", "ivc_entropy.hip")], check=True)
 print("variant:", VARIANT or "(default)")
 sys.path.insert(0, ROOT)
 import ivclab_amd._native as N  # noqa: E402  (shares torch's HIP runtime)
