@@ -464,7 +464,7 @@ def main():
         torch.cuda.empty_cache()
 
     if rank == 0 and not args.no_cpu:
-        host = intra_frames(40, H, W, seed=3, dev=dev).cpu().numpy()
+        host = intra_frames(80, H, W, seed=3, dev=dev).cpu().numpy()
         mpx, n, dt = cpu_baseline_intra(host)
         result["cpu_baseline"] = {
             "value": round(mpx, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",

@@ -8,7 +8,8 @@ import json
 import sys
 
 
-def main(summary, frames, H, W, out, match="fused_encode_kernel<unsigned char"):
+def main(summary, frames, H, W, out,
+         match="fused_encode_kernel<unsigned char, double, double, 1, true, false, 0,"):
     d = json.load(open(summary))
     name = next(k for k in d if match in k)
     rec = d[name]
