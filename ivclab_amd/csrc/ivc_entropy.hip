@@ -166,7 +166,10 @@ __device__ __forceinline__ uint32_t popc_below(uint64_t mask) {
 }
 
 // blocks handled per wave-iteration (independent loads in flight)
-constexpr int ZR_UNROLL = 4;
+#ifndef IVC_ZR_UNROLL
+#define IVC_ZR_UNROLL 4
+#endif
+constexpr int ZR_UNROLL = IVC_ZR_UNROLL;
 
 __global__ __launch_bounds__(256) void zr_count_kernel(const int32_t* __restrict__ src,
                                                        int64_t nblk, int stride, int B,
@@ -246,12 +249,271 @@ static unsigned zr_grid(int64_t nblk) {
   return (unsigned)(grid < 1 ? 1 : grid);
 }
 
+// ---- wide path: dense 64-coefficient rows (block_size = row stride = 64, 16-B aligned) --
+// A wave takes ZW_BLK consecutive blocks per iteration with 16-byte loads: lane l holds
+// coefficients 4(l%16) .. 4(l%16)+3 of block l/16 of each 4-block load.  A block's 64-bit
+// nonzero mask is the OR over its 16 lanes of their nibbles (4 xor-shuffles), so every lane
+// knows its block's mask, run starts and symbol count (same rules as zr_mask).  Emission
+// assembles the ZW_BLK blocks' contiguous symbol range in the wave's LDS and stores it with
+// consecutive-address whole-wave dword stores.
+constexpr int ZW_LOADS = 4, ZW_BLK = 4 * ZW_LOADS;
+constexpr int ZW_MAXSYM = 97;                 // symbols of a 64-coefficient block, at most
+constexpr int ZW_STAGE = ZW_BLK * ZW_MAXSYM;  // int32 per wave
+
+typedef int32_t zv4 __attribute__((ext_vector_type(4)));
+
+struct ZwMask {
+  uint64_t m, st;
+  int cnt;
+};
+
+__device__ __forceinline__ ZwMask zw_mask(zv4 x, int lane) {
+  const uint32_t nib = (uint32_t)(x.x != 0) | (uint32_t)(x.y != 0) << 1 |
+                       (uint32_t)(x.z != 0) << 2 | (uint32_t)(x.w != 0) << 3;
+  unsigned long long m = (unsigned long long)nib << (4 * (lane & 15));
+#pragma unroll
+  for (int d = 1; d < 16; d <<= 1) m |= __shfl_xor(m, d);
+  ZwMask z;
+  z.m = m;
+  const int last = m ? 63 - __builtin_clzll(m) : -1;
+  const uint64_t inside = last < 0 ? 0ull : (last == 63 ? ~0ull : ((1ull << (last + 1)) - 1));
+  const uint64_t zeros = ~z.m & inside;
+  z.st = zeros & ~(zeros << 1);
+  z.cnt = __builtin_popcountll(z.m) + 2 * __builtin_popcountll(z.st) + 1;
+  return z;
+}
+
+__device__ __forceinline__ zv4 zw_load(const int32_t* src, int64_t nblk, int64_t b0, int u,
+                                        int lane) {
+  const int64_t blk = b0 + 4 * u + (lane >> 4);
+  if (blk >= nblk) return zv4{0, 0, 0, 0};
+  return __builtin_nontemporal_load(reinterpret_cast<const zv4*>(src + blk * 64) + (lane & 15));
+}
+
+__global__ __launch_bounds__(256) void zw_count_kernel(const int32_t* __restrict__ src, int64_t nblk,
+                                                       int32_t* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t b0 = wave * ZW_BLK; b0 < nblk; b0 += nw * ZW_BLK) {
+    zv4 x[ZW_LOADS];
+#pragma unroll
+    for (int u = 0; u < ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
+#pragma unroll
+    for (int u = 0; u < ZW_LOADS; ++u) {
+      const ZwMask z = zw_mask(x[u], lane);
+      const int64_t blk = b0 + 4 * u + (lane >> 4);
+      if ((lane & 15) == 0 && blk < nblk) counts[blk] = z.cnt;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict__ src, int64_t nblk,
+                                                      int32_t eob, const int64_t* __restrict__ off,
+                                                      int32_t* __restrict__ out, int64_t capacity) {
+  __shared__ int32_t stage[4 * ZW_STAGE];
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  int32_t* zs = stage + (threadIdx.x >> 6) * ZW_STAGE;
+  const int i = lane & 15;
+  const uint64_t low = i == 0 ? 0ull : (~0ull >> (64 - 4 * i));   // positions below 4i
+  for (int64_t b0 = wave * ZW_BLK; b0 < nblk; b0 += nw * ZW_BLK) {
+    zv4 x[ZW_LOADS];
+#pragma unroll
+    for (int u = 0; u < ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
+    const int64_t bend = b0 + ZW_BLK < nblk ? b0 + ZW_BLK : nblk;
+    const int64_t wbase = off[b0], wend = off[bend];
+#pragma unroll
+    for (int u = 0; u < ZW_LOADS; ++u) {
+      const ZwMask z = zw_mask(x[u], lane);
+      const int64_t blk = b0 + 4 * u + (lane >> 4);
+      if (blk < nblk) {
+        int p = (int)(off[blk] - wbase) + __builtin_popcountll(z.m & low) +
+                2 * __builtin_popcountll(z.st & low);
+        const int32_t v[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int pos = 4 * i + j;
+          if ((z.m >> pos) & 1ull) {
+            zs[p] = v[j];
+            p += 1;
+          } else if ((z.st >> pos) & 1ull) {
+            zs[p] = 0;
+            zs[p + 1] = __builtin_ctzll(z.m >> pos);   // run ends before the last nonzero
+            p += 2;
+          }
+        }
+        if (i == 0) zs[(int)(off[blk] - wbase) + z.cnt - 1] = eob;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // the ZW_BLK blocks' symbols are the contiguous range [wbase, wend); written while they
+    // fit the caller's capacity
+    const int n = (int)(wend - wbase);
+    const int64_t lim = capacity - wbase;
+    for (int k = lane; k < n; k += 64)
+      if (k < lim) out[wbase + k] = zs[k];
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+static bool zw_ok(const int32_t* src, int stride, int B) {
+  return stride == 64 && B == 64 && ((uintptr_t)src & 15u) == 0;
+}
+
+static unsigned zw_grid(int64_t nblk, int per_cu) {
+  const int64_t waves = (nblk + ZW_BLK - 1) / ZW_BLK;
+  int64_t grid = (waves + 3) / 4;
+  if (grid > 256 * per_cu) grid = 256 * per_cu;
+  return (unsigned)(grid < 1 ? 1 : grid);
+}
+
+// ---- single pass (dense rows, device API): the coefficients are read once.  A wave takes
+// 16-block tiles in order from an atomic counter, publishes the tile's symbol count, looks
+// back over its predecessors' published words (decoupled look-back: a tile publishes its
+// count before it looks back itself, so no wave ever waits on a wave that is waiting), then
+// publishes its inclusive prefix and emits the tile exactly as zw_emit_kernel does.
+// Status word of a tile: bits 62-63 = 0 not ready, 1 count only, 2 inclusive prefix.
+constexpr uint64_t ZS_AGG = 1ull << 62, ZS_INCL = 2ull << 62, ZS_VAL = ZS_AGG - 1;
+
+__device__ __forceinline__ uint64_t zs_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void zs_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// exclusive symbol offset of `tile` (> 0): lane k reads the word of tile base - k; the nearest
+// inclusive word ends the walk, count-only words before it add up, a not-ready word among
+// them makes the wave read the window again
+__device__ int64_t zs_lookback(const uint64_t* status, int64_t tile, int lane) {
+  int64_t excl = 0, base = tile - 1;
+  while (true) {
+    const int64_t t = base - lane;
+    const uint64_t w = t >= 0 ? zs_load(status + t) : ZS_INCL;    // before tile 0: prefix 0
+    const uint64_t incl = __ballot((w >> 62) == 2);
+    const uint64_t notready = __ballot((w >> 62) == 0);
+    const int first = incl ? __builtin_ctzll(incl) : 63;
+    const uint64_t need = first == 63 ? ~0ull : ((2ull << first) - 1);   // lanes 0..first
+    if (notready & need) {
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    long long v = lane <= first ? (long long)(w & ZS_VAL) : 0;
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+    excl += v;
+    if (incl) return excl;
+    base -= 64;
+  }
+}
+
+__global__ __launch_bounds__(256) void zs_encode_kernel(const int32_t* __restrict__ src, int64_t nblk,
+                                                        int32_t eob, uint64_t* __restrict__ status,
+                                                        unsigned long long* __restrict__ next_tile,
+                                                        int64_t* __restrict__ off,
+                                                        int32_t* __restrict__ out, int64_t capacity) {
+  __shared__ int32_t stage[4 * ZW_STAGE];
+  const int lane = threadIdx.x & 63;
+  int32_t* zs = stage + (threadIdx.x >> 6) * ZW_STAGE;
+  const int i = lane & 15, seg = lane >> 4;
+  const uint64_t low = i == 0 ? 0ull : (~0ull >> (64 - 4 * i));   // positions below 4i
+  const int64_t ntiles = (nblk + ZW_BLK - 1) / ZW_BLK;
+  while (true) {
+    unsigned long long tk = 0;
+    if (lane == 0) tk = atomicAdd(next_tile, 1ull);
+    const int64_t tile = (int64_t)__shfl((long long)tk, 0);
+    if (tile >= ntiles) break;
+    const int64_t b0 = tile * ZW_BLK;
+    zv4 x[ZW_LOADS];
+#pragma unroll
+    for (int u = 0; u < ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
+    ZwMask z[ZW_LOADS];
+#pragma unroll
+    for (int u = 0; u < ZW_LOADS; ++u) z[u] = zw_mask(x[u], lane);
+    // the tile's block counts (block 4u + s on lanes 16s..16s+15) and their prefix, in scalars
+    int pre[ZW_BLK + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int u = 0; u < ZW_LOADS; ++u)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int b = 4 * u + s;
+        const int c = b0 + b < nblk ? __builtin_amdgcn_readlane(z[u].cnt, 16 * s) : 0;
+        pre[b + 1] = pre[b] + c;
+      }
+    const int agg = pre[ZW_BLK];
+    if (lane == 0) zs_store(status + tile, (tile == 0 ? ZS_INCL : ZS_AGG) | (uint64_t)agg);
+    const int64_t wbase = tile == 0 ? 0 : zs_lookback(status, tile, lane);
+    if (tile > 0 && lane == 0) zs_store(status + tile, ZS_INCL | (uint64_t)(wbase + agg));
+#pragma unroll
+    for (int u = 0; u < ZW_LOADS; ++u) {
+      const int64_t blk = b0 + 4 * u + seg;
+      const int lb = seg == 0 ? pre[4 * u] : seg == 1 ? pre[4 * u + 1]
+                   : seg == 2 ? pre[4 * u + 2] : pre[4 * u + 3];      // block's tile offset
+      if (blk < nblk) {
+        int p = lb + __builtin_popcountll(z[u].m & low) + 2 * __builtin_popcountll(z[u].st & low);
+        const int32_t v[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int pos = 4 * i + j;
+          if ((z[u].m >> pos) & 1ull) {
+            zs[p] = v[j];
+            p += 1;
+          } else if ((z[u].st >> pos) & 1ull) {
+            zs[p] = 0;
+            zs[p + 1] = __builtin_ctzll(z[u].m >> pos);   // run ends before the last nonzero
+            p += 2;
+          }
+        }
+        if (i == 0) {
+          zs[lb + z[u].cnt - 1] = eob;
+          off[blk] = wbase + lb;
+        }
+      }
+    }
+    if (tile == ntiles - 1 && lane == 0) off[nblk] = wbase + agg;
+    __builtin_amdgcn_wave_barrier();
+    const int64_t lim = capacity - wbase;
+    for (int k = lane; k < agg; k += 64)
+      if (k < lim) out[wbase + k] = zs[k];
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// bytes of device scratch the single-pass encoder needs (tile status words + the tile counter)
+int64_t zerorun_single_pass_scratch_bytes(int64_t nblk) {
+  return ((nblk + ZW_BLK - 1) / ZW_BLK + 1) * 8;
+}
+
+// the single pass applies to dense, 16-B aligned 64-coefficient rows; returns
+// hipErrorNotSupported otherwise (the caller then runs the two-pass path)
+hipError_t launch_zerorun_single_pass(const int32_t* src, int64_t nblk, int stride, int B,
+                                      int32_t eob, int64_t* off, int32_t* out, int64_t capacity,
+                                      void* scratch, hipStream_t s) {
+  if (!zw_ok(src, stride, B)) return hipErrorNotSupported;
+  if (nblk <= 0) return hipMemsetAsync(off, 0, sizeof(int64_t), s);
+  const int64_t ntiles = (nblk + ZW_BLK - 1) / ZW_BLK;
+  hipError_t e = hipMemsetAsync(scratch, 0, (size_t)(ntiles + 1) * 8, s);
+  if (e != hipSuccess) return e;
+  uint64_t* status = (uint64_t*)scratch;
+  const unsigned grid = resident_grid_ptr(reinterpret_cast<const void*>(zs_encode_kernel),
+                                          (ntiles + 3) / 4);
+  zs_encode_kernel<<<grid, 256, 0, s>>>(src, nblk, eob, status,
+                                        (unsigned long long*)(status + ntiles), off, out, capacity);
+  return hipGetLastError();
+}
+
 // off[0..nblk]: exclusive symbol offsets of the blocks, off[nblk] = stream length.
 // Scratch: counts int32[nblk], agg int64[scan_scratch_elems(nblk)].
 hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, int B,
                                   int32_t* counts, int64_t* agg, int64_t* off, hipStream_t s) {
   if (nblk <= 0) return hipMemsetAsync(off, 0, sizeof(int64_t), s);
-  zr_count_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, counts);
+  if (zw_ok(src, stride, B))
+    zw_count_kernel<<<zw_grid(nblk, 8), 256, 0, s>>>(src, nblk, counts);
+  else
+    zr_count_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, counts);
   return device_scan<int64_t>(nblk, CountGen{counts}, SumI64{}, OffsetSink{off, nblk}, agg, s);
 }
 
@@ -267,7 +529,10 @@ hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* 
 hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
                                const int64_t* off, int32_t* out, int64_t capacity, hipStream_t s) {
   if (nblk <= 0) return hipSuccess;
-  zr_emit_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, eob, off, out, capacity);
+  if (zw_ok(src, stride, B))
+    zw_emit_kernel<<<zw_grid(nblk, 6), 256, 0, s>>>(src, nblk, eob, off, out, capacity);
+  else
+    zr_emit_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, eob, off, out, capacity);
   return hipGetLastError();
 }
 
@@ -427,14 +692,38 @@ __global__ void minmax_init(int32_t* mm) {
   mm[1] = INT32_MIN;
 }
 
+// 16 B per lane, 4 loads in flight (after an unaligned head; the tail by workgroup 0)
 __global__ __launch_bounds__(256) void minmax_kernel(const int32_t* __restrict__ sym, int64_t n,
                                                      int32_t* mm) {
   int32_t lo = INT32_MAX, hi = INT32_MIN;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const int32_t v = __builtin_nontemporal_load(sym + i);
+  auto see = [&](int32_t v) {
     lo = v < lo ? v : lo;
     hi = v > hi ? v : hi;
+  };
+  const int tid = threadIdx.x;
+  int64_t head = (int64_t)(((16u - ((uintptr_t)sym & 15u)) & 15u) / 4u);
+  if (head > n) head = n;
+  if (blockIdx.x == 0 && tid < head) see(sym[tid]);
+  sym += head;
+  n -= head;
+  typedef int32_t v4 __attribute__((ext_vector_type(4)));
+  const v4* sv = reinterpret_cast<const v4*>(sym);
+  const int64_t nv = n / 4, stride = (int64_t)gridDim.x * 256;
+  int64_t i = (int64_t)blockIdx.x * 256 + tid;
+  for (; i + 3 * stride < nv; i += 4 * stride) {
+    v4 x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load(sv + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      see(x[u].x); see(x[u].y); see(x[u].z); see(x[u].w);
+    }
   }
+  for (; i < nv; i += stride) {
+    const v4 x = __builtin_nontemporal_load(sv + i);
+    see(x.x); see(x.y); see(x.z); see(x.w);
+  }
+  if (blockIdx.x == 0 && tid < (int)(n - nv * 4)) see(sym[nv * 4 + tid]);
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     const int32_t ol = __shfl_xor(lo, d), oh = __shfl_xor(hi, d);
@@ -451,7 +740,7 @@ hipError_t launch_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm, hipStre
   minmax_init<<<1, 1, 0, s>>>(mm);
   if (n > 0) {
     int64_t g = (n + 256 * 64 - 1) / (256 * 64);
-    if (g > 256 * 8) g = 256 * 8;
+    if (g > 256 * 4) g = 256 * 4;
     minmax_kernel<<<(unsigned)g, 256, 0, s>>>(sym, n, mm);
   }
   return hipGetLastError();

@@ -1318,9 +1318,23 @@ hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t
 }
 
 // ======================================================================================
-// Symbol histogram (feeds stats_marg / the Huffman table, entropy.py:6-29): per-workgroup
-// LDS bins, the dominant zero symbol counted by wave ballots, one global add per bin.
+// Symbol histogram (feeds stats_marg / the Huffman table, entropy.py:6-29).  Zero-run and
+// coefficient streams are concentrated near zero (the cfg3 stream: values -3..4 are 89% of
+// the symbols, 1 alone 29%), so a wave's LDS atomics on one bin serialise ~20-way.  Each
+// thread therefore counts the HOT values -3..4 in registers (one compare-add per counter,
+// flushed once through a wave reduction and the same clamp as every other value) and only
+// the rest go to per-workgroup LDS bins; one global add per bin per workgroup at the end.
 // ======================================================================================
+constexpr int HIST_HOT_LO = -3, HIST_HOT_N = 8, HIST_UNROLL = 4;
+
+template <typename S>
+__device__ __forceinline__ int hist_bin(S v, int64_t lo, int32_t nbins) {
+  // clamp into the end bins; v - lo is formed unsigned once v > lo (no overflow)
+  if ((int64_t)v <= lo) return 0;
+  if ((uint64_t)(int64_t)v - (uint64_t)lo >= (uint64_t)nbins) return nbins - 1;
+  return (int)((uint64_t)(int64_t)v - (uint64_t)lo);
+}
+
 template <typename S>
 __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sym, int64_t n,
                                                         int64_t lo, int32_t nbins,
@@ -1332,22 +1346,18 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
     for (int i = tid; i < nbins; i += 256) bins[i] = 0;
     __syncthreads();
   }
-  // the bin of symbol value 0 (the dominant symbol) is counted per thread, added once
-  const uint64_t nlo = (uint64_t)0 - (uint64_t)lo;   // -lo without overflow
-  const int zb = lo > 0 ? 0 : (nlo >= (uint64_t)nbins ? nbins - 1 : (int)nlo);
-  unsigned zeros = 0;
+  uint32_t hot[HIST_HOT_N];
+#pragma unroll
+  for (int k = 0; k < HIST_HOT_N; ++k) hot[k] = 0;
   auto count = [&](S v) {
-    // clamp into the end bins; v - lo is formed unsigned once v > lo (no overflow)
-    int b;
-    if ((int64_t)v <= lo) b = 0;
-    else if ((uint64_t)(int64_t)v - (uint64_t)lo >= (uint64_t)nbins) b = nbins - 1;
-    else b = (int)((uint64_t)(int64_t)v - (uint64_t)lo);
-    if (b == zb) {
-      ++zeros;
-    } else if (use_lds) {
-      atomicAdd(&bins[b], 1u);
+    const uint64_t u = (uint64_t)((int64_t)v - (int64_t)HIST_HOT_LO);
+    if (u < (uint64_t)HIST_HOT_N) {
+#pragma unroll
+      for (int k = 0; k < HIST_HOT_N; ++k) hot[k] += u == (uint64_t)k ? 1u : 0u;
     } else {
-      atomicAdd(&hist[b], 1ull);
+      const int b = hist_bin(v, lo, nbins);
+      if (use_lds) atomicAdd(&bins[b], 1u);
+      else atomicAdd(&hist[b], 1ull);
     }
   };
   // a stream that does not start on 16 B: the first `head` symbols apart
@@ -1357,32 +1367,47 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
   if (blockIdx.x == 0 && tid < head) count(sym[tid]);
   sym += head;
   n -= head;
-  // 16 B per lane, two loads in flight per iteration (the symbol stream is read once)
+  // 16 B per lane, HIST_UNROLL loads in flight per iteration (the stream is read once)
   typedef S vec_t __attribute__((ext_vector_type(PER)));
   const vec_t* sv = reinterpret_cast<const vec_t*>(sym);
   const int64_t nv = n / PER, stride = (int64_t)gridDim.x * 256;
   int64_t i = (int64_t)blockIdx.x * 256 + tid;
-  for (; i + stride < nv; i += 2 * stride) {
-    const vec_t a = __builtin_nontemporal_load(sv + i);
-    const vec_t b = __builtin_nontemporal_load(sv + i + stride);
+  for (; i + (HIST_UNROLL - 1) * stride < nv; i += HIST_UNROLL * stride) {
+    vec_t x[HIST_UNROLL];
 #pragma unroll
-    for (int k = 0; k < PER; ++k) count(a[k]);
+    for (int u = 0; u < HIST_UNROLL; ++u) x[u] = __builtin_nontemporal_load(sv + i + u * stride);
 #pragma unroll
-    for (int k = 0; k < PER; ++k) count(b[k]);
+    for (int u = 0; u < HIST_UNROLL; ++u)
+#pragma unroll
+      for (int k = 0; k < PER; ++k) count(x[u][k]);
   }
-  if (i < nv) {
+  for (; i < nv; i += stride) {
     const vec_t a = __builtin_nontemporal_load(sv + i);
 #pragma unroll
     for (int k = 0; k < PER; ++k) count(a[k]);
   }
   if (blockIdx.x == 0 && tid < (int)(n - nv * PER)) count(sym[nv * PER + tid]);
+  // hot counters: wave sums, added by lane 0 to the (clamped) bin of each hot value
+#pragma unroll
+  for (int k = 0; k < HIST_HOT_N; ++k) {
+    uint32_t c = hot[k];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+    hot[k] = c;
+  }
+  if ((tid & 63) == 0) {
+#pragma unroll
+    for (int k = 0; k < HIST_HOT_N; ++k) {
+      if (!hot[k]) continue;
+      const int b = hist_bin((S)(HIST_HOT_LO + k), lo, nbins);
+      if (use_lds) atomicAdd(&bins[b], hot[k]);
+      else atomicAdd(&hist[b], (unsigned long long)hot[k]);
+    }
+  }
   if (use_lds) {
-    atomicAdd(&bins[zb], zeros);
     __syncthreads();
     for (int i2 = tid; i2 < nbins; i2 += 256)
       if (bins[i2]) atomicAdd(&hist[i2], (unsigned long long)bins[i2]);
-  } else if (zeros) {
-    atomicAdd(&hist[zb], (unsigned long long)zeros);
   }
 }
 

@@ -416,6 +416,14 @@ def test_histogram_device_offsets_and_ragged(dt):
             h = torch.zeros(512, dtype=torch.int64, device="cuda")
             D.histogram(t[off:off + n], -256, h)
             assert np.array_equal(h.cpu().numpy(), O.histogram(base[off:off + n], -256, 512)), (off, n)
+    # the register-counted values -3..4 landing in clamped end bins, bins starting inside them,
+    # a one-bin histogram, and more than 16384 bins (global atomics instead of LDS)
+    hot = rng.integers(-6, 8, 1 << 18).astype(dt)
+    th = torch.from_numpy(hot).cuda()
+    for lo, nb in ((2, 3), (-1, 2), (0, 1), (-3, 8), (-100, 20000), (5, 4)):
+        h = torch.zeros(nb, dtype=torch.int64, device="cuda")
+        D.histogram(th, lo, h)
+        assert np.array_equal(h.cpu().numpy(), O.histogram(hot, lo, nb)), (lo, nb)
 
 
 # ------------------------------------------------------------------------ device API ---
@@ -572,6 +580,51 @@ def test_zerorun_device_api_and_capacity():
     assert np.array_equal(dec.cpu().numpy(), x)
 
 
+@pytest.mark.parametrize("nblk", [1, 15, 16, 17, 1023, 1024 * 16 + 5, 300001])
+def test_zerorun_device_single_pass(nblk):
+    """The device encoder's single pass (dense 64-coefficient rows: 16-block tiles, decoupled
+    look-back over the tiles' published counts) against the oracle: tile-ragged ends, more
+    tiles than one 64-word look-back window, truncated capacity, and a view that is not
+    16-B aligned (two-pass path) for comparison."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(nblk)
+    x = rng.integers(-40, 41, (nblk, 64)).astype(np.int32)
+    x[rng.random((nblk, 64)) > rng.random((nblk, 1))] = 0
+    x[::7] = 0                                   # all-zero blocks: EOB only
+    x[3::11] = rng.integers(1, 5, (len(x[3::11]), 64))   # no zeros: 65 symbols
+    want = O.zerorun_encode_fast(x)
+    blocks = torch.from_numpy(x).cuda()
+    off = torch.full((nblk + 1,), -7, dtype=torch.int64, device="cuda")
+    out = torch.full((want.size + 3,), -1, dtype=torch.int32, device="cuda")
+    D.zerorun_encode(blocks, off, out)
+    torch.cuda.synchronize()
+    # per-block symbol counts: nonzeros + 2 per zero run before the last nonzero + EOB
+    nz = x != 0
+    last = np.where(nz.any(1), 63 - np.argmax(nz[:, ::-1], axis=1), -1)
+    zeros = ~nz & (np.arange(64)[None] <= last[:, None])
+    starts = zeros & ~np.concatenate([np.zeros((nblk, 1), bool), zeros[:, :-1]], axis=1)
+    cnt = nz.sum(1) + 2 * starts.sum(1) + 1
+    o = off.cpu().numpy()
+    assert np.array_equal(o, np.concatenate([[0], np.cumsum(cnt)])) and o[-1] == want.size
+    got = out.cpu().numpy()
+    assert np.array_equal(got[:want.size], want) and (got[want.size:] == -1).all()
+    cap = want.size // 3
+    short = torch.full((cap,), -1, dtype=torch.int32, device="cuda")
+    D.zerorun_encode(blocks, off, short)
+    torch.cuda.synchronize()
+    assert int(off[-1]) == want.size
+    assert np.array_equal(short.cpu().numpy(), want[:cap])
+    # the same blocks one int32 off a 16-B boundary take the two-pass path
+    buf = torch.zeros(nblk * 64 + 1, dtype=torch.int32, device="cuda")
+    buf[1:] = blocks.view(-1)
+    off2 = torch.empty(nblk + 1, dtype=torch.int64, device="cuda")
+    out2 = torch.empty(want.size, dtype=torch.int32, device="cuda")
+    D.zerorun_encode(buf[1:].view(nblk, 64), off2, out2)
+    torch.cuda.synchronize()
+    assert torch.equal(off2, off) and np.array_equal(out2.cpu().numpy(), want)
+
+
 def test_zerorun_after_fused_intra():
     """The codec chain: fused intra encode with zig-zag -> zero-run stream -> decode ->
     back to the quantised blocks, against the oracle's chain."""
@@ -605,6 +658,20 @@ def test_minmax_host_and_device():
         dm = torch.zeros(2, dtype=torch.int32, device="cuda")
         D.minmax(t, dm)
         assert dm.cpu().tolist() == list(map(int, want))
+    # views starting off 16 B, lengths around the vector/unroll edges, extremes in the head,
+    # the body and the tail
+    base = rng.integers(-1000, 1000, (1 << 20) + 11).astype(np.int32)
+    tb = torch.from_numpy(base).cuda()
+    for off in (0, 1, 2, 3):
+        for n in (1, 3, 4, 5, 17, 4099, 1 << 16, (1 << 20) + 11 - off):
+            for pos in (0, n // 2, n - 1):
+                v = base[off:off + n].copy()
+                v[pos] = -5000 if pos != n - 1 else 5000
+                tb[off:off + n] = torch.from_numpy(v).cuda()
+                dm = torch.zeros(2, dtype=torch.int32, device="cuda")
+                D.minmax(tb[off:off + n], dm)
+                assert dm.cpu().tolist() == [int(v.min()), int(v.max())], (off, n, pos)
+                tb[off:off + n] = torch.from_numpy(base[off:off + n]).cuda()
 
 
 def _zr_chain(img, table, scale=None):
