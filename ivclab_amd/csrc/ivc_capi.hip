@@ -611,21 +611,6 @@ int ivc_zerorun_encode_dev(const int32_t* src, int64_t nblk, int32_t row_stride,
   TRY(check_zr(nblk, row_stride, block_size));
   CHECK(capacity >= 0, IVC_E_ARG, "zerorun: capacity must be >= 0");
   hipStream_t s = (hipStream_t)stream;
-#ifndef IVC_ZR_SINGLE
-#define IVC_ZR_SINGLE 1
-#endif
-  if (IVC_ZR_SINGLE && nblk > 0 && block_size == 64 && row_stride == 64 &&
-      ((uintptr_t)src & 15u) == 0) {
-    // dense 64-coefficient rows: one pass over the coefficients (decoupled look-back)
-    void* scratch = nullptr;
-    hipError_t e = scratch_alloc(&scratch, (size_t)zerorun_single_pass_scratch_bytes(nblk), s);
-    if (e != hipSuccess) return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
-    const int rc = dev_launch(launch_zerorun_single_pass(src, nblk, row_stride, block_size, eob, offsets,
-                                                         out, capacity, scratch, s),
-                              "zerorun_encode");
-    (void)hipFreeAsync(scratch, s);
-    return rc;
-  }
   int32_t* counts = nullptr;
   int64_t* agg = nullptr;
   if (nblk > 0) {

@@ -369,142 +369,6 @@ static unsigned zw_grid(int64_t nblk, int per_cu) {
   return (unsigned)(grid < 1 ? 1 : grid);
 }
 
-// ---- single pass (dense rows, device API): the coefficients are read once.  A wave takes
-// 16-block tiles in order from an atomic counter, publishes the tile's symbol count, looks
-// back over its predecessors' published words (decoupled look-back: a tile publishes its
-// count before it looks back itself, so no wave ever waits on a wave that is waiting), then
-// publishes its inclusive prefix and emits the tile exactly as zw_emit_kernel does.
-// Status word of a tile: bits 62-63 = 0 not ready, 1 count only, 2 inclusive prefix.
-constexpr uint64_t ZS_AGG = 1ull << 62, ZS_INCL = 2ull << 62, ZS_VAL = ZS_AGG - 1;
-
-__device__ __forceinline__ uint64_t zs_load(const uint64_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void zs_store(uint64_t* p, uint64_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// exclusive symbol offset of `tile` (> 0): lane k reads the word of tile base - k; the nearest
-// inclusive word ends the walk, count-only words before it add up, a not-ready word among
-// them makes the wave read the window again
-__device__ int64_t zs_lookback(const uint64_t* status, int64_t tile, int lane) {
-  int64_t excl = 0, base = tile - 1;
-  while (true) {
-    const int64_t t = base - lane;
-    const uint64_t w = t >= 0 ? zs_load(status + t) : ZS_INCL;    // before tile 0: prefix 0
-    const uint64_t incl = __ballot((w >> 62) == 2);
-    const uint64_t notready = __ballot((w >> 62) == 0);
-    const int first = incl ? __builtin_ctzll(incl) : 63;
-    const uint64_t need = first == 63 ? ~0ull : ((2ull << first) - 1);   // lanes 0..first
-    if (notready & need) {
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    long long v = lane <= first ? (long long)(w & ZS_VAL) : 0;
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-    excl += v;
-    if (incl) return excl;
-    base -= 64;
-  }
-}
-
-__global__ __launch_bounds__(256) void zs_encode_kernel(const int32_t* __restrict__ src, int64_t nblk,
-                                                        int32_t eob, uint64_t* __restrict__ status,
-                                                        unsigned long long* __restrict__ next_tile,
-                                                        int64_t* __restrict__ off,
-                                                        int32_t* __restrict__ out, int64_t capacity) {
-  __shared__ int32_t stage[4 * ZW_STAGE];
-  const int lane = threadIdx.x & 63;
-  int32_t* zs = stage + (threadIdx.x >> 6) * ZW_STAGE;
-  const int i = lane & 15, seg = lane >> 4;
-  const uint64_t low = i == 0 ? 0ull : (~0ull >> (64 - 4 * i));   // positions below 4i
-  const int64_t ntiles = (nblk + ZW_BLK - 1) / ZW_BLK;
-  while (true) {
-    unsigned long long tk = 0;
-    if (lane == 0) tk = atomicAdd(next_tile, 1ull);
-    const int64_t tile = (int64_t)__shfl((long long)tk, 0);
-    if (tile >= ntiles) break;
-    const int64_t b0 = tile * ZW_BLK;
-    zv4 x[ZW_LOADS];
-#pragma unroll
-    for (int u = 0; u < ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
-    ZwMask z[ZW_LOADS];
-#pragma unroll
-    for (int u = 0; u < ZW_LOADS; ++u) z[u] = zw_mask(x[u], lane);
-    // the tile's block counts (block 4u + s on lanes 16s..16s+15) and their prefix, in scalars
-    int pre[ZW_BLK + 1];
-    pre[0] = 0;
-#pragma unroll
-    for (int u = 0; u < ZW_LOADS; ++u)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int b = 4 * u + s;
-        const int c = b0 + b < nblk ? __builtin_amdgcn_readlane(z[u].cnt, 16 * s) : 0;
-        pre[b + 1] = pre[b] + c;
-      }
-    const int agg = pre[ZW_BLK];
-    if (lane == 0) zs_store(status + tile, (tile == 0 ? ZS_INCL : ZS_AGG) | (uint64_t)agg);
-    const int64_t wbase = tile == 0 ? 0 : zs_lookback(status, tile, lane);
-    if (tile > 0 && lane == 0) zs_store(status + tile, ZS_INCL | (uint64_t)(wbase + agg));
-#pragma unroll
-    for (int u = 0; u < ZW_LOADS; ++u) {
-      const int64_t blk = b0 + 4 * u + seg;
-      const int lb = seg == 0 ? pre[4 * u] : seg == 1 ? pre[4 * u + 1]
-                   : seg == 2 ? pre[4 * u + 2] : pre[4 * u + 3];      // block's tile offset
-      if (blk < nblk) {
-        int p = lb + __builtin_popcountll(z[u].m & low) + 2 * __builtin_popcountll(z[u].st & low);
-        const int32_t v[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int pos = 4 * i + j;
-          if ((z[u].m >> pos) & 1ull) {
-            zs[p] = v[j];
-            p += 1;
-          } else if ((z[u].st >> pos) & 1ull) {
-            zs[p] = 0;
-            zs[p + 1] = __builtin_ctzll(z[u].m >> pos);   // run ends before the last nonzero
-            p += 2;
-          }
-        }
-        if (i == 0) {
-          zs[lb + z[u].cnt - 1] = eob;
-          off[blk] = wbase + lb;
-        }
-      }
-    }
-    if (tile == ntiles - 1 && lane == 0) off[nblk] = wbase + agg;
-    __builtin_amdgcn_wave_barrier();
-    const int64_t lim = capacity - wbase;
-    for (int k = lane; k < agg; k += 64)
-      if (k < lim) out[wbase + k] = zs[k];
-    __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// bytes of device scratch the single-pass encoder needs (tile status words + the tile counter)
-int64_t zerorun_single_pass_scratch_bytes(int64_t nblk) {
-  return ((nblk + ZW_BLK - 1) / ZW_BLK + 1) * 8;
-}
-
-// the single pass applies to dense, 16-B aligned 64-coefficient rows; returns
-// hipErrorNotSupported otherwise (the caller then runs the two-pass path)
-hipError_t launch_zerorun_single_pass(const int32_t* src, int64_t nblk, int stride, int B,
-                                      int32_t eob, int64_t* off, int32_t* out, int64_t capacity,
-                                      void* scratch, hipStream_t s) {
-  if (!zw_ok(src, stride, B)) return hipErrorNotSupported;
-  if (nblk <= 0) return hipMemsetAsync(off, 0, sizeof(int64_t), s);
-  const int64_t ntiles = (nblk + ZW_BLK - 1) / ZW_BLK;
-  hipError_t e = hipMemsetAsync(scratch, 0, (size_t)(ntiles + 1) * 8, s);
-  if (e != hipSuccess) return e;
-  uint64_t* status = (uint64_t*)scratch;
-  const unsigned grid = resident_grid_ptr(reinterpret_cast<const void*>(zs_encode_kernel),
-                                          (ntiles + 3) / 4);
-  zs_encode_kernel<<<grid, 256, 0, s>>>(src, nblk, eob, status,
-                                        (unsigned long long*)(status + ntiles), off, out, capacity);
-  return hipGetLastError();
-}
-
 // off[0..nblk]: exclusive symbol offsets of the blocks, off[nblk] = stream length.
 // Scratch: counts int32[nblk], agg int64[scan_scratch_elems(nblk)].
 hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, int B,

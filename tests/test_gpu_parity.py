@@ -581,11 +581,11 @@ def test_zerorun_device_api_and_capacity():
 
 
 @pytest.mark.parametrize("nblk", [1, 15, 16, 17, 1023, 1024 * 16 + 5, 300001])
-def test_zerorun_device_single_pass(nblk):
-    """The device encoder's single pass (dense 64-coefficient rows: 16-block tiles, decoupled
-    look-back over the tiles' published counts) against the oracle: tile-ragged ends, more
-    tiles than one 64-word look-back window, truncated capacity, and a view that is not
-    16-B aligned (two-pass path) for comparison."""
+def test_zerorun_device_wide_and_general(nblk):
+    """The device encoder's wide path (dense, 16-B aligned 64-coefficient rows: 16 blocks per
+    wave-iteration) against the oracle and an independent per-block count: ends that are not
+    a multiple of 16 blocks, all-zero and zero-free blocks, truncated capacity; then the same
+    blocks one int32 off a 16-B boundary (general one-block-per-wave path)."""
     torch = pytest.importorskip("torch")
     import ivclab_amd.device as D
     rng = np.random.default_rng(nblk)
@@ -615,7 +615,7 @@ def test_zerorun_device_single_pass(nblk):
     torch.cuda.synchronize()
     assert int(off[-1]) == want.size
     assert np.array_equal(short.cpu().numpy(), want[:cap])
-    # the same blocks one int32 off a 16-B boundary take the two-pass path
+    # the same blocks one int32 off a 16-B boundary take the general path
     buf = torch.zeros(nblk * 64 + 1, dtype=torch.int32, device="cuda")
     buf[1:] = blocks.view(-1)
     off2 = torch.empty(nblk + 1, dtype=torch.int64, device="cuda")
