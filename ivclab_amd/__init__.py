@@ -10,7 +10,7 @@ reference's NumPy/SciPy results bit for bit; there is no CPU fallback.
     from ivclab_amd.quantization import PatchQuant
     from ivclab_amd.utils import ZigZag, Patcher
     from ivclab_amd.signal.zigzag import zigzag_scan
-    from ivclab_amd.video import MotionCompensator
+    from ivclab_amd.video import MotionCompensator, VideoCodec
     from ivclab_amd.entropy import ZeroRunCoder
 
 `install_as_ivclab()` registers these modules under the reference's import paths
@@ -25,7 +25,7 @@ from .signal import DiscreteCosineTransform  # noqa: F401
 from .utils import Patcher, ZigZag  # noqa: F401
 from .entropy import HuffmanCoder, ZeroRunCoder  # noqa: F401
 from .image import IntraCodec  # noqa: F401
-from .video import MotionCompensator  # noqa: F401
+from .video import MotionCompensator, VideoCodec  # noqa: F401
 
 __version__ = "0.1.0"
 
@@ -41,6 +41,7 @@ _ALIASES = {
     "ivclab.utils.metrics": "ivclab_amd.utils.metrics",
     "ivclab.video": "ivclab_amd.video",
     "ivclab.video.motion": "ivclab_amd.video.motion",
+    "ivclab.video.videocodec": "ivclab_amd.video.videocodec",
     "ivclab.entropy": "ivclab_amd.entropy",
     "ivclab.entropy.huffman": "ivclab_amd.entropy.huffman",
     "ivclab.image": "ivclab_amd.image",
@@ -62,5 +63,5 @@ def install_as_ivclab() -> None:
         parent, _, leaf = name.rpartition(".")
         setattr(sys.modules[parent], leaf, mod)
     for cls in (PatchQuant, DiscreteCosineTransform, Patcher, ZigZag, MotionCompensator,
-                ZeroRunCoder, HuffmanCoder, IntraCodec):
+                ZeroRunCoder, HuffmanCoder, IntraCodec, VideoCodec):
         setattr(root, cls.__name__, cls)

@@ -843,6 +843,36 @@ def test_intracodec_encode_decode_roundtrip():
     assert np.array_equal(codec.intra_decode(bs, img.shape), rec)
 
 
+def test_videocodec_iframe_and_pframe():
+    """VideoCodec (videocodec.py:37-86): frame 0 is the oracle chain on the luma plane
+    (rgb2ycbcr of the float32 frame, the 3-plane quantisation of a grayscale input, the
+    first plane of the 3-channel reconstruction clipped into Y, ycbcr2rgb, uint8); its bit
+    count is the Huffman code lengths of the frame's symbols.  Frame 1 raises ValueError as
+    the reference does: the motion-vector coder trained on [-40, 40] meets indices up to 80."""
+    from ivclab_amd.video import VideoCodec
+    rng = np.random.default_rng(31)
+    scale = 0.8
+    frame = rng.integers(0, 256, (32, 48, 3)).astype(np.uint8)
+    codec = VideoCodec(quantization_scale=scale)
+    rec, bitstream, bits = codec.encode_decode(frame, frame_num=0)
+    ycc = O.rgb2ycbcr_fma(frame.astype(np.float32))
+    y = ycc[..., 0]
+    sym = _chain_symbols(y, scale)
+    rec_y = _chain_image(sym, y.shape, scale)
+    assert rec_y.shape == (32, 48, 3) and codec.decoder_recon.shape == (32, 48, 3)
+    assert_bits(codec.decoder_recon, rec_y, "I-frame luma reconstruction")
+    want = ycc.copy()
+    want[..., 0] = np.clip(rec_y[..., 0], 0, 255)
+    assert_bits(rec, O.ycbcr2rgb(want).astype(np.uint8), "I-frame RGB")
+    L = codec.intra_codec.huffman.encoder_codebook
+    assert bits == float(L[sym - codec.intra_codec.bounds[0]].astype(np.int64).sum())
+    nxt = np.roll(frame, (2, -3), axis=(0, 1))
+    mv = O.motion_vectors(codec.decoder_recon[..., 0], O.rgb2ycbcr_fma(nxt.astype(np.float32))[..., 0], 4)
+    assert mv.max() > 40
+    with pytest.raises(ValueError, match="outside the trained range"):
+        codec.encode_decode(nxt, frame_num=1)
+
+
 def test_stats_marg_gpu_vs_oracle():
     """stats_marg on the GPU histogram equals np.histogram's counts (dropped out-of-range
     values, closed last bin) divided by the sample count."""
