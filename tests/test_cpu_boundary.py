@@ -125,6 +125,8 @@ def test_install_as_ivclab():
         from ivclab.utils import Patcher, ZigZag  # noqa: F401
         from ivclab.utils.metrics import calc_mse
         from ivclab.video import MotionCompensator  # noqa: F401
+        from ivclab.video.videocodec import VideoCodec
+        assert VideoCodec is IA.VideoCodec
         assert DiscreteCosineTransform is IA.DiscreteCosineTransform
         assert PatchQuant is IA.PatchQuant
         assert calc_mse(np.zeros((2, 2, 3)), np.ones((2, 2, 3))) == 1.0
