@@ -327,6 +327,43 @@ def test_intra_encode_distinct_chroma_planes(dtype, zz):
         assert_bits(out[f], want, f"frame {f}")
 
 
+def test_cfg1_512_gray_through_the_classes():
+    """BASELINE configs[0] (default_rng(0), 512x512x1 u8): Patcher.patch ->
+    DCT.transform -> PatchQuant.quantize through the drop-in classes, and the fused kernel,
+    bit-exact against the oracle; then dequantize -> inverse_transform -> unpatch."""
+    N, L = _native()
+    img = np.random.default_rng(0).integers(0, 256, (512, 512, 1), dtype=np.uint8)
+    P, D, Q = Patcher(), DiscreteCosineTransform(), PatchQuant(1.0)
+    q = Q.quantize(D.transform(P.patch(img)))
+    want = O.quantize(O.dct_transform(O.patch(img)), 1.0)
+    assert q.shape == (64, 64, 3, 8, 8)
+    assert_bits(q, want, "cfg1 classes")
+    t = N.table_arg(Q.get_quantization_table())
+    fused = np.empty((1, 64, 64, 3, 64), np.int32)
+    N.check(L.ivc_intra_encode(N.ptr(np.ascontiguousarray(img[None])), 1, 1, 512, 512, 1, N.ptr(t),
+                               N.F64, 0, N.ptr(fused)))
+    assert_bits(fused[0], want.reshape(64, 64, 3, 64), "cfg1 fused")
+    rec = P.unpatch(D.inverse_transform(Q.dequantize(q)))
+    assert_bits(rec, O.unpatch(O.dct_inverse(O.dequantize(want, 1.0))), "cfg1 inverse")
+
+
+def test_cfg2_1080p_rgb_per_channel_with_zigzag():
+    """BASELINE configs[1] (default_rng(1), 1920x1080 RGB u8): per-channel DCT +
+    quantise + zig-zag through the classes and the fused kernel (C = 3), bit-exact."""
+    N, L = _native()
+    img = np.random.default_rng(1).integers(0, 256, (1080, 1920, 3), dtype=np.uint8)
+    P, D, Q, Z = Patcher(), DiscreteCosineTransform(), PatchQuant(1.0), ZigZag()
+    zz = Z.flatten(Q.quantize(D.transform(P.patch(img))))
+    want = O.zigzag_flatten(O.quantize(O.dct_transform(O.patch(img)), 1.0))
+    assert zz.shape == (135, 240, 3, 64)
+    assert_bits(zz, want, "cfg2 classes")
+    t = N.table_arg(Q.get_quantization_table())
+    fused = np.empty((1, 135, 240, 3, 64), np.int32)
+    N.check(L.ivc_intra_encode(N.ptr(np.ascontiguousarray(img[None])), 1, 1, 1080, 1920, 3, N.ptr(t),
+                               N.F64, 1, N.ptr(fused)))
+    assert_bits(fused[0], want, "cfg2 fused")
+
+
 def test_intra_encode_4k_full_frame():
     """One full cfg3 frame (3840x2160 luma) bit-exact against the oracle."""
     N, L = _native()
