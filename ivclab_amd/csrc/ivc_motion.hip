@@ -258,6 +258,10 @@ static unsigned me_fast_grid(const void* kernel, int64_t wgs) {
   return (unsigned)(g < wgs ? g : wgs);
 }
 
+#ifndef IVC_ME_XCD
+#define IVC_ME_XCD 1
+#endif
+
 template <int SR> struct MeCfg;
 // PITCH: LDS row pitch of a staged window (dwords), chosen so a row read of a 32-lane half
 // hits distinct banks (searched offline; SR = 4 is 2-way at best with 4 blocks per wave)
@@ -370,7 +374,12 @@ __global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restri
         rc, okc ? (8 * by + (c >> 1)) * W + 8 * (bx0 + blk) + 4 * (c & 1) : 0x40000000, 0, 0);
   };
 
-  uint32_t grp = blockIdx.x * 4u + wave;
+  // XCD-aware order: workgroups are dealt round-robin over the 8 XCDs (b and b + 8 share
+  // one), so logical workgroup (b % 8) * (G / 8) + b / 8 gives each XCD a contiguous run of
+  // groups: adjacent blocks, whose windows and S2 rows overlap, then share one L2
+  uint32_t wg = blockIdx.x;
+  if (IVC_ME_XCD && (gridDim.x & 7u) == 0u) wg = (wg & 7u) * (gridDim.x >> 3) + (wg >> 3);
+  uint32_t grp = wg * 4u + wave;
   uint32_t wraw[PW], craw;
   fetch(grp, grp < ngroups, wraw, craw);
   for (; grp < ngroups; grp += nwaves) {

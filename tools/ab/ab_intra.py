@@ -23,6 +23,7 @@ ap.add_argument("--frames", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--inter", action="store_true")
+ap.add_argument("--inter-shape", default="300x1080x1920", help="frames x H x W of the inter A/B")
 ap.add_argument("--pace", default="", help="comma-separated store-pace rates (GB/s, 0 = off) "
                 "to time for every library that exports ivc_set_store_pace")
 ap.add_argument("--trace-pace", type=int, default=0,
@@ -115,7 +116,8 @@ del img
 torch.cuda.empty_cache()
 
 if args.inter:
-    Fi, Hi, Wi, sr = 300, 1080, 1920, 16
+    Fi, Hi, Wi = map(int, args.inter_shape.split("x"))
+    sr = 16
     seq = bench.inter_frames(Fi, Hi, Wi, seed=4, dev=dev)
     mvs = [torch.empty((Fi - 1, Hi // 8, Wi // 8), dtype=torch.int64, device=dev) for _ in libs]
     qs = [torch.empty((Fi - 1, Hi // 8, Wi // 8, 3, 64), dtype=torch.int32, device=dev) for _ in libs]
