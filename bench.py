@@ -271,6 +271,11 @@ def main():
     ap.add_argument("--no-cpu-pool", action="store_true", help="skip the multi-core CPU leg")
     ap.add_argument("--sharded-frames", type=int, default=120)
     ap.add_argument("--sharded-steps", type=int, default=3)
+    ap.add_argument("--sharded-hist-wg", type=int, default=2,
+                    help="workgroups per CU of the side-stream histograms in the cfg5 step")
+    ap.add_argument("--sharded-chunk", type=int, default=8,
+                    help="frame pairs per inter_encode call in the cfg5 step; the histogram of "
+                         "chunk k runs on a side stream while chunk k+1 is encoded (0: one call)")
     args = ap.parse_args()
 
     dist, rank, world, local = dist_setup(args.gpus)
@@ -428,6 +433,7 @@ def main():
     # ---- cfg5: 8K x 120 frames, frame-sharded ME + DCT, one all-gather of histograms ------
     if not args.no_sharded:
         from ivclab_amd.distributed import shard_pairs
+        from ivclab_amd import _native as N
         F5, H5, W5, sr5 = args.sharded_frames, 4320, 7680, 16
         a5, b5 = shard_pairs(F5, rank, world)          # this rank's frames incl. the halo
         n5 = max(b5 - a5, 0)
@@ -438,14 +444,29 @@ def main():
         nmv = (2 * sr5 + 1) ** 2
         hist5 = torch.zeros(HIST_BINS + nmv, dtype=torch.int64, device=dev)
 
+        side = torch.cuda.Stream(device=dev)
+        ck = args.sharded_chunk if args.sharded_chunk > 0 else max(pairs5, 1)
+
         def sstep():
             # the step: ME + MC + residual DCT + quantise of this rank's pairs, then the
-            # symbol histograms (coefficients | MV indices) and their all-gather
+            # symbol histograms (coefficients | MV indices) and their all-gather.  The pairs
+            # go in chunks of `ck`: ME is VALU-bound and the histogram HBM-bound, so chunk k's
+            # histograms run on a side stream while chunk k+1 is encoded (same work, same
+            # counts: integer adds in one stream order)
+            main = torch.cuda.current_stream()
+            L = N.lib()
+            prev_wg = L.ivc_histogram_occupancy()
+            N.check(L.ivc_set_histogram_occupancy(args.sharded_hist_wg))
             hist5.zero_()
-            if pairs5:
-                D.inter_encode(seq5, sr5, table, mv5, q5, zigzag=args.zigzag)
-                D.histogram(q5.view(-1), HIST_LO, hist5[:HIST_BINS])
-                D.histogram(mv5.view(-1), 0, hist5[HIST_BINS:])
+            for p0 in range(0, pairs5, ck):
+                p1 = min(p0 + ck, pairs5)
+                D.inter_encode(seq5[p0:p1 + 1], sr5, table, mv5[p0:p1], q5[p0:p1],
+                               zigzag=args.zigzag, stream=main)
+                side.wait_stream(main)
+                D.histogram(q5[p0:p1].view(-1), HIST_LO, hist5[:HIST_BINS], stream=side)
+                D.histogram(mv5[p0:p1].view(-1), 0, hist5[HIST_BINS:], stream=side)
+            main.wait_stream(side)
+            N.check(L.ivc_set_histogram_occupancy(prev_wg))
             return global_histogram(hist5)
 
         swall, _ = timed(dist, sstep, args.sharded_steps, 1)
@@ -464,7 +485,10 @@ def main():
                          if dist is not None else "none (1 rank)",
                          "bins": HIST_BINS + nmv,
                          "symbols": int(g5[:HIST_BINS].sum().item()),
-                         "motion_vectors": int(g5[HIST_BINS:].sum().item())},
+                         "motion_vectors": int(g5[HIST_BINS:].sum().item()),
+                         "hist_checksum": int((g5 * torch.arange(1, g5.numel() + 1, device=dev))
+                                              .sum().item())},
+            "chunk_pairs": ck,
         }
         del seq5, mv5, q5
         torch.cuda.empty_cache()

@@ -179,6 +179,13 @@ int ivc_histogram_i32_dev(const int32_t* sym, int64_t n, int32_t lo, int32_t nbi
 int ivc_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist);
 int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
                           int64_t* hist, void* stream);
+/* Workgroups per CU of the histogram launches (default 4, which fills the chip; 0 restores
+ * the default).  A histogram on a side stream next to a VALU-bound kernel (the frame-sharded
+ * bench step overlaps chunk k's histogram with chunk k+1's motion search) runs better with
+ * 1-2, leaving LDS and wave slots to the other stream.  Timing only: counts are identical.
+ * No reference counterpart.                                                               */
+int ivc_set_histogram_occupancy(int wg_per_cu);
+int ivc_histogram_occupancy(void);
 
 /* ---------------------------------------------------------------- colour ----------- */
 /* rgb2ycbcr (ivclab/signal/color.py:15-38): npix pixels of 3 channels (any dtype) ->

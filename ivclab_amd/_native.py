@@ -44,6 +44,8 @@ _SIGS = {
     "ivc_set_store_pace": ([_ct.c_double], _I),
     "ivc_store_pace": ([], _ct.c_double),
     "ivc_store_pace_late": ([], _ct.c_double),
+    "ivc_set_histogram_occupancy": ([_I], _I),
+    "ivc_histogram_occupancy": ([], _I),
     "ivc_dct8x8": ([_P, _I, _L, _P, _I, _I, _I], _I),
     "ivc_dct8x8_dev": ([_P, _I, _L, _P, _I, _I, _I, _P], _I),
     "ivc_quantize": ([_P, _I, _L, _I, _P, _I, _P], _I),

@@ -205,6 +205,15 @@ double ivc_store_pace(void) { return store_pace_gbps(); }
 
 double ivc_store_pace_late(void) { return store_pace_late_fraction(); }
 
+int ivc_set_histogram_occupancy(int wg_per_cu) {
+  if (wg_per_cu < 0 || wg_per_cu > 16)
+    return fail(IVC_E_ARG, "ivc_set_histogram_occupancy: wg_per_cu must be in [0, 16]");
+  set_histogram_wg_per_cu(wg_per_cu);
+  return IVC_OK;
+}
+
+int ivc_histogram_occupancy(void) { return histogram_wg_per_cu(); }
+
 int ivc_release_scratch(void) {
   int dev = 0;
   TRY(current_device(&dev));

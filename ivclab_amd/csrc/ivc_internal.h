@@ -42,6 +42,9 @@ hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, in
 double store_pace_gbps();
 double store_pace_late_fraction();
 void set_store_pace_gbps(double gbps);
+// workgroups per CU of the histogram launches (ivc_kernels.hip)
+int histogram_wg_per_cu();
+void set_histogram_wg_per_cu(int k);
 unsigned resident_grid_ptr(const void* kernel, int64_t work_groups_needed);
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 // zero-run coding (ivc_entropy.hip)

@@ -1411,13 +1411,19 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
   }
 }
 
+// workgroups per CU of the histogram launches: 4 fills the chip (the stream alone is
+// HBM-bound); fewer leave LDS and wave slots to kernels on other streams
+static int g_hist_wg_per_cu = 4;
+int histogram_wg_per_cu() { return g_hist_wg_per_cu; }
+void set_histogram_wg_per_cu(int k) { g_hist_wg_per_cu = k > 0 ? k : 4; }
+
 template <typename S>
 static hipError_t launch_hist(const S* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist,
                               hipStream_t s) {
   if (n <= 0 || nbins <= 0) return hipSuccess;
   const int use_lds = nbins <= 16384;
   const size_t lds = use_lds ? (size_t)nbins * 4 : 0;
-  histogram_kernel<S><<<grid_for(n, 256 * 16, 4), 256, lds, s>>>(
+  histogram_kernel<S><<<grid_for(n, 256 * 16, g_hist_wg_per_cu), 256, lds, s>>>(
       sym, n, lo, nbins, reinterpret_cast<unsigned long long*>(hist), use_lds);
   return hipGetLastError();
 }

@@ -424,6 +424,34 @@ def test_histogram_vs_oracle():
         assert np.array_equal(h, O.histogram(sym, lo, nb))
 
 
+def test_histogram_occupancy_changes_timing_only():
+    """ivc_set_histogram_occupancy (workgroups per CU) leaves the counts unchanged, on the
+    caller's stream next to another stream's work; 0 restores the default, > 16 is refused."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    N, L = _native()
+    rng = np.random.default_rng(5)
+    sym = rng.integers(-300, 300, (1 << 22) + 3).astype(np.int32)
+    sym[::2] = 0
+    want = O.histogram(sym, -2048, 4096)
+    s = torch.from_numpy(sym).cuda()
+    side = torch.cuda.Stream()
+    start = L.ivc_histogram_occupancy()
+    try:
+        for k in (1, 2, 16, 0):
+            N.check(L.ivc_set_histogram_occupancy(k))
+            assert L.ivc_histogram_occupancy() == (k or 4)
+            h = torch.zeros(4096, dtype=torch.int64, device="cuda")
+            side.wait_stream(torch.cuda.current_stream())
+            D.histogram(s, -2048, h, stream=side)
+            torch.cuda.current_stream().wait_stream(side)
+            assert np.array_equal(h.cpu().numpy(), want), k
+        assert L.ivc_set_histogram_occupancy(17) == N.E_ARG
+        assert L.ivc_set_histogram_occupancy(-1) == N.E_ARG
+    finally:
+        N.check(L.ivc_set_histogram_occupancy(start))
+
+
 def test_histogram_i64_vs_oracle():
     """int64 symbols (motion-vector indices): host entry point, values beyond both ends."""
     N, L = _native()
