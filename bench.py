@@ -5,26 +5,44 @@ of 256 synthetic 3840x2160 luma frames per GPU, resident in HBM, through the fus
 patch -> DCT-II -> quantise kernel (reference-equivalent output: [F,270,480,3,64] int32, the
 C = 1 -> 3-plane broadcast of patchquant.py:59).  One step = one pass over the batch.
 `roofline` prices that kernel against HBM (13 B/px algorithmic, HIP events on its stream;
-`traffic` from the committed PMC record), `cpu_baseline` times the reference's algorithm
-(oracle) on one host core, `cpu_baseline_multicore` on the box's cores.
+`traffic` = the rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE record of this very libivc.so build, or
+null), `cpu_baseline` times the reference's algorithm (oracle) on one host core,
+`cpu_baseline_multicore` on every core the box grants this process.
 
-Also reported from the same run:
+Also reported from the same run (each with its own timing; none of them is `value`):
   zerorun / image2symbols  ZeroRunCoder on the zig-zag output, and pixels -> symbols fused
   exchange                 global Huffman-table input: alphabet bounds (all-reduce) and the
                            symbol histogram (all-gather), as IntraCodec trains it
-  inter                    configs[3]: 1080p x 300, +-16 full-search ME + MC + residual DCT+quant
+  inter                    configs[3]: 1080p x 300, +-16 full-search ME + MC + residual
+                           DCT+quant; `roofline` of the motion search (dot4-VALU bound)
+  inter_f64                the ME VideoCodec really runs: NumPy-semantics float64 SSD
+                           (pairwise order) on non-integer 1080p luma, +-16; FP64-VALU roofline
+  class_api                host buffers through the drop-in classes (DCT.transform ->
+                           PatchQuant.quantize -> ZigZag.flatten) and the one-call host entry
+                           point, PCIe included: a 4K luma frame and configs[1] (1080p RGB)
   sharded                  configs[4]: 8K x 120 frames split across the ranks (strong scaling),
                            ME + residual DCT+quant + one histogram all-gather per step
-Multi-GPU: one process per GPU (torch.distributed, RCCL); cfg3/cfg4 are weak-scaled (each
-rank owns its frames), cfg5 strong-scaled.
+`verify` (default on; --no-verify skips it) checks sampled outputs of every timed leg against
+the oracle after its timed region — the oracle is the checker there, never what is timed —
+and recomputes the cfg5 histograms in one unsharded, unchunked run on rank 0.
+
+Multi-GPU: one process per GPU (torch.distributed, backend nccl = RCCL).  Under torchrun
+(WORLD_SIZE set) the ranks come from the environment and must number --gpus; without it,
+`--gpus N` (N > 1) starts N ranks itself through torch.distributed.run (127.0.0.1) before
+anything touches the GPU, and exits with their status.  cfg3/cfg4 are weak-scaled (each rank
+owns its frames), cfg5 strong-scaled.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--no-inter] [--no-cpu]
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,14 +53,36 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
-INT_VALU_PEAK_TOPS = 78.6      # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz, 32-bit integer ops/s
+# VALU peaks, 256 CUs x 4 SIMDs x 64 lanes at 2.4 GHz:
+#   v_dot4_u32_u8 issues at half rate (tools/ubench/valu_rates.hip): 39.3 T lane-instr/s
+#   FP64 add/mul (no FMA: NumPy rounds every product): half the FP32 vector rate, 39.3 T op/s
+DOT4_PEAK_T = 256 * 4 * 64 * 2.4e9 / 4 / 1e12
+F64_PEAK_T = 78.6 / 2
 HIST_LO, HIST_BINS = -4096, 8192
+METRIC = "Mpixels/s: 4K intra DCT+quant and ±16 full-search ME, 1/2/4/8 MI355X"
+
+
+# ---------------------------------------------------------------- ranks -----------------
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(n, argv, port):
+    """torch.distributed.run command that starts n ranks of this script with the same
+    arguments (the driver's own launch form)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__)] + list(argv)
 
 
 def dist_setup(n_gpus):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}")
     if world > 1:
         import torch.distributed as dist
         # rehearsal of the multi-rank path on a 1-GPU box: IVC_BENCH_BACKEND=gloo puts every
@@ -69,13 +109,21 @@ def barrier(dist):
         dist.barrier()
 
 
-def max_over_ranks(dist, v):
+def _reduce(dist, v, op):
     if dist is None:
         return v
     t = torch.tensor([v], dtype=torch.float64,
                      device="cpu" if dist.get_backend() == "gloo" else "cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=op)
     return float(t.item())
+
+
+def max_over_ranks(dist, v):
+    return v if dist is None else _reduce(dist, v, dist.ReduceOp.MAX)
+
+
+def min_over_ranks(dist, v):
+    return v if dist is None else _reduce(dist, v, dist.ReduceOp.MIN)
 
 
 # ---------------------------------------------------------------- synthetic frames ------
@@ -126,10 +174,18 @@ def inter_frames(F, H, W, seed, dev, first=0):
     return out
 
 
+def luma_f64(frames_u8):
+    """Non-integer float64 luma of the u8 sequence, the kind VideoCodec hands the motion
+    search (rgb2ycbcr(frame.astype(float32))[..., 0], videocodec.py:38,52): the Y row of
+    color.py's matrix applied to a grey pixel, plus the 16 offset."""
+    return frames_u8.to(torch.float64) * (0.299 + 0.587 + 0.114) * (219.0 / 255.0) + 16.0
+
+
 # ---------------------------------------------------------------- timing ----------------
 def timed(dist, fn, steps, warmup):
     """W untimed steps, then exactly K steps bracketed by barrier + synchronize; returns
-    (max-over-ranks wall seconds, per-step device-event ms of fn's kernels)."""
+    (max-over-ranks wall seconds, per-step device-event ms of fn's kernels on the current
+    stream)."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
@@ -148,6 +204,49 @@ def timed(dist, fn, steps, warmup):
     return wall, ev0.elapsed_time(ev1) / steps
 
 
+def valid_candidates(h_px, w_px, sr):
+    """Exact count of in-frame candidates of an [h_px, w_px] frame's 8x8 blocks at +-sr
+    (motion.py:41-43)."""
+    by, bx, d = np.arange(h_px // 8) * 8, np.arange(w_px // 8) * 8, np.arange(-sr, sr + 1)
+    vy = ((by[:, None] + d[None]) >= 0) & ((by[:, None] + d[None] + 8) <= h_px)
+    vx = ((bx[:, None] + d[None]) >= 0) & ((bx[:, None] + d[None] + 8) <= w_px)
+    return int(vy.sum(1).sum() * vx.sum(1).sum())
+
+
+def lib_sha256():
+    from ivclab_amd import _native as N
+    with open(N.LIB_PATH, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()
+
+
+# ---------------------------------------------------------------- CPU baselines ---------
+def cpu_share():
+    """Cores this process may use on the box: the affinity mask, capped by the cgroup CPU
+    quota when one is set.  Returns (cores, affinity, quota or None)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    n = aff if quota is None else max(1, min(aff, int(math.floor(quota + 1e-9))))
+    return n, aff, quota
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as fh:
+            for line in fh:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline_intra(frames_host, budget_s=12.0):
     """Oracle (NumPy/SciPy restatement of the reference, single thread, as the reference
     runs) on whole 4K frames until ~budget_s of CPU work; returns Mpx/s and frames done."""
@@ -163,200 +262,110 @@ def cpu_baseline_intra(frames_host, budget_s=12.0):
     return n * H * W / dt / 1e6, n, dt
 
 
-def cpu_baseline_me(frames_host, sr, budget_s=10.0):
+def cpu_baseline_me(frames_host, sr):
     """The reference's literal ME loop (oracle motion_vectors_loop on float64 frames) on a
     stripe of block rows of one 1080p pair, extrapolated per valid candidate."""
     from oracle import ivc_oracle as O
     a = frames_host[0].astype(np.float64)
     b = frames_host[1].astype(np.float64)
     H, W = a.shape
-    # a 32-row sub-frame from the middle of the pair (4 block rows x W)
-    sub_h = 32
+    sub_h = 32                                   # 4 block rows from the middle of the pair
     y0 = (H // 2) // 8 * 8
-    ra, rb = a[y0:y0 + sub_h], b[y0:y0 + sub_h]
     t0 = time.perf_counter()
-    O.motion_vectors_loop(ra, rb, sr)
+    O.motion_vectors_loop(a[y0:y0 + sub_h], b[y0:y0 + sub_h], sr)
     dt = time.perf_counter() - t0
-    n = 2 * sr + 1
-
-    def valid_count(h, w):
-        by = np.arange(h // 8) * 8
-        bx = np.arange(w // 8) * 8
-        d = np.arange(-sr, sr + 1)
-        vy = ((by[:, None] + d[None]) >= 0) & ((by[:, None] + d[None] + 8) <= h)
-        vx = ((bx[:, None] + d[None]) >= 0) & ((bx[:, None] + d[None] + 8) <= w)
-        return int(vy.sum(1).sum() * vx.sum(1).sum())
-
-    per_cand = dt / valid_count(sub_h, W)
-    frame_s = per_cand * valid_count(H, W)
-    return H * W / frame_s / 1e6, per_cand, n
-
-
-def cpu_workers():
-    """Host cores this process may use (the GPU box's share, not the whole machine)."""
-    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
-    return max(1, min(n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16))
-
-
-def cpu_model():
-    try:
-        with open("/proc/cpuinfo") as fh:
-            for line in fh:
-                if line.startswith("model name"):
-                    return line.split(":", 1)[1].strip()
-    except OSError:
-        pass
-    return "unknown"
+    per_cand = dt / valid_candidates(sub_h, W, sr)
+    return H * W / (per_cand * valid_candidates(H, W, sr)) / 1e6, per_cand
 
 
 def cpu_baseline_pool(intra_host, me_pair, sr, budget_s=8.0):
-    """The same oracle paths frame-sharded over the host cores (multiprocessing, spawn):
-    intra on whole frames (each worker its own frames) and the ME loop on block-row
-    stripes (each worker its own stripe).  Returns (intra Mpx/s, ME Mpx/s, workers)."""
+    """The same oracle paths frame-sharded over every core the box grants (multiprocessing,
+    spawn): intra on whole frames (each worker its own frames) and the ME loop on block-row
+    stripes (each worker its own stripe).  Returns (intra Mpx/s, ME Mpx/s, workers, share)."""
     import multiprocessing as mp
     from oracle import cpu_pool
-    P = cpu_workers()
+    P, aff, quota = cpu_share()
     ctx = mp.get_context("spawn")
     with ctx.Pool(P) as pool:
         pool.map(cpu_pool.warm, range(P))
-        # intra: 1 frame per worker per round until the budget is spent
         H, W = intra_host[0].shape
         done, t0 = 0, time.perf_counter()
         while time.perf_counter() - t0 < budget_s / 2:
             chunks = [[intra_host[(done + i) % len(intra_host)]] for i in range(P)]
             done += sum(pool.map(cpu_pool.intra_frames, chunks))
         intra_mpx = done * H * W / (time.perf_counter() - t0) / 1e6
-        # ME: P stripes of 16 rows (2 block rows) from the middle of a 1080p pair
+        # ME: P stripes of 16 rows (2 block rows) from the middle of a 1080p pair (stripes
+        # wrap round the frame when P is large)
         a = me_pair[0].astype(np.float64)
         b = me_pair[1].astype(np.float64)
         Hm, Wm = a.shape
-        y0 = (Hm // 2 - 8 * P) // 8 * 8
-        stripes = [(a[y0 + 16 * i:y0 + 16 * i + 16], b[y0 + 16 * i:y0 + 16 * i + 16], sr)
-                   for i in range(P)]
+        nstripe = Hm // 16
+        stripes = [(a[16 * (i % nstripe):16 * (i % nstripe) + 16],
+                    b[16 * (i % nstripe):16 * (i % nstripe) + 16], sr) for i in range(P)]
         t0 = time.perf_counter()
         pool.map(cpu_pool.me_stripe, stripes)
         dt = time.perf_counter() - t0
-    # per-candidate rate of the stripes, extrapolated to whole frames like the 1-core leg
-    n = 2 * sr + 1
-
-    def valid(h, w):
-        by, bx, d = np.arange(h // 8) * 8, np.arange(w // 8) * 8, np.arange(-sr, sr + 1)
-        vy = ((by[:, None] + d[None]) >= 0) & ((by[:, None] + d[None] + 8) <= h)
-        vx = ((bx[:, None] + d[None]) >= 0) & ((bx[:, None] + d[None] + 8) <= w)
-        return int(vy.sum(1).sum() * vx.sum(1).sum())
-
-    del n
-    cand_rate = P * valid(16, Wm) / dt
-    me_mpx = Hm * Wm / (valid(Hm, Wm) / cand_rate) / 1e6
-    return intra_mpx, me_mpx, P
+    cand_rate = P * valid_candidates(16, Wm, sr) / dt
+    me_mpx = Hm * Wm / (valid_candidates(Hm, Wm, sr) / cand_rate) / 1e6
+    return intra_mpx, me_mpx, P, {"affinity": aff, "cgroup_quota": quota}
 
 
-# ---------------------------------------------------------------- main ------------------
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=6)
-    ap.add_argument("--frames", type=int, default=256)
-    ap.add_argument("--height", type=int, default=2160)
-    ap.add_argument("--width", type=int, default=3840)
-    ap.add_argument("--inter-frames", type=int, default=300)
-    ap.add_argument("--inter-steps", type=int, default=3)
-    ap.add_argument("--sr", type=int, default=16)
-    ap.add_argument("--zigzag", action="store_true")
-    ap.add_argument("--no-inter", action="store_true")
-    ap.add_argument("--no-intra", action="store_true", help="profiling aid: skip the cfg3 leg")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-sharded", action="store_true", help="skip the cfg5 8K leg")
-    ap.add_argument("--no-cpu-pool", action="store_true", help="skip the multi-core CPU leg")
-    ap.add_argument("--sharded-frames", type=int, default=120)
-    ap.add_argument("--sharded-steps", type=int, default=3)
-    ap.add_argument("--sharded-hist-wg", type=int, default=2,
-                    help="workgroups per CU of the side-stream histograms in the cfg5 step")
-    ap.add_argument("--sharded-chunk", type=int, default=8,
-                    help="frame pairs per inter_encode call in the cfg5 step; the histogram of "
-                         "chunk k runs on a side stream while chunk k+1 is encoded (0: one call)")
-    args = ap.parse_args()
+# ---------------------------------------------------------------- verification ----------
+def check_equal(got, want, what, failures):
+    got, want = np.asarray(got), np.asarray(want)
+    ok = got.dtype == want.dtype and got.shape == want.shape and got.tobytes() == want.tobytes()
+    if not ok:
+        failures.append(what)
+    return ok
 
-    dist, rank, world, local = dist_setup(args.gpus)
-    dev = torch.device("cuda", torch.cuda.current_device())
+
+# ---------------------------------------------------------------- legs ------------------
+def leg_intra(args, dist, rank, world, dev, table, result, verify):
     import ivclab_amd.device as D
-    from ivclab_amd.distributed import global_bounds, global_histogram
-    from ivclab_amd.entropy.stats import (entropy_bits, huffman_bounds, smooth_pmf,
-                                          stats_marg_from_counts)
-    from ivclab_amd import PatchQuant
-    table = PatchQuant(1.0).get_quantization_table()
-
-    # ---- cfg3: 4K intra DCT + quant -------------------------------------------------------
+    from ivclab_amd import _native as N
     F, H, W = args.frames, args.height, args.width
-    if args.no_intra:
-        F = 1
     frames = intra_frames(F, H, W, seed=3 + 1000 * rank, dev=dev).view(F, H, W, 1)
     out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
 
     def step():
         D.intra_encode(frames, table, out, zigzag=args.zigzag)
 
+    L = N.lib()
     wall, kern_ms = timed(dist, step, args.steps, args.warmup)
-    from ivclab_amd import _native as N
-    pace_rate, pace_late = N.lib().ivc_store_pace(), N.lib().ivc_store_pace_late()
-
+    pace = {"total_GBs": round(L.ivc_store_pace(), 1),
+            "late_fraction_last": round(L.ivc_store_pace_late(), 4)}
+    st = N.pace_stats()
+    if st is not None:
+        pace.update(st)
     # write-stream ceiling for this buffer: the same 12 B/px of int32 output written by
     # torch's vectorised fill kernel (no reads) — what the store side alone can reach
     _, fill_ms = timed(None, lambda: out.fill_(0), 3, 1)
     fill_gbs = out.numel() * 4 / (fill_ms * 1e-3) / 1e9
+    if verify is not None:
+        step()
+        torch.cuda.synchronize()
+        from oracle import ivc_oracle as O
+        picks = sorted({0, F // 2, F - 1})
+        for f in picks:
+            want = O.intra_encode(frames[f].cpu().numpy(), 1.0, zigzag=args.zigzag)
+            check_equal(out[f].cpu().numpy(), want.reshape(out.shape[1:]), f"intra frame {f}",
+                        verify["failures"])
+        verify["checked"].append(f"intra: frames {picks} of {F} (rank {rank}) whole vs oracle")
     px_step = F * H * W
     value = world * px_step * args.steps / wall / 1e6
     algo_bytes = px_step * 13                        # 1 B u8 in + 3 x 4 B int32 out per px
     achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
-
-    # ---- symbols for the global Huffman table (IntraCodec.image2symbols + training input,
-    # intracodec.py:32-90,149-166): the same frames with zig-zag, zero-run coded on the GPU;
-    # global alphabet bounds (one all-reduce), per-rank histogram, one all-gather
-    D.intra_encode(frames, table, out, zigzag=True)
-    nblk = out.numel() // 64
-    blocks = out.view(nblk, 64)
-    offs = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
-    probe = torch.empty(1, dtype=torch.int32, device=dev)
-    D.zerorun_encode(blocks, offs, probe)
-    nsym = int(offs[-1].item())
-    sym = torch.empty(nsym, dtype=torch.int32, device=dev)
-    zwall, zms = timed(dist, lambda: D.zerorun_encode(blocks, offs, sym), 3, 1)
-    # the same stream straight from the pixels (fused: the coefficients never reach HBM)
-    nsym_d = torch.zeros(1, dtype=torch.int64, device=dev)
-    fwall, fms = timed(dist, lambda: D.intra_symbols(frames, table, sym, nsym_d), 3, 1)
-    fused_same = bool(int(nsym_d.item()) == nsym)
-    mm = torch.empty(2, dtype=torch.int32, device=dev)
-
-    def exchange():
-        D.minmax(sym, mm)
-        lo, hi = global_bounds(mm)
-        b0, b1 = huffman_bounds(lo, hi)
-        hist = torch.zeros(b1 - b0 - 1, dtype=torch.int64, device=dev)
-        D.histogram(sym, b0, hist)
-        return b0, b1, global_histogram(hist)
-
-    exchange()                      # warm-up: first-launch and allocator costs stay untimed
-    torch.cuda.synchronize()
-    barrier(dist)
-    t_ex = time.perf_counter()
-    b0, b1, ghist = exchange()
-    torch.cuda.synchronize()
-    exchange_ms = (time.perf_counter() - t_ex) * 1e3
-    counts = ghist.cpu().numpy()
-    total_syms = int(counts.sum())
-    pmf = smooth_pmf(stats_marg_from_counts(counts))
-    del sym, offs, blocks
-    traffic = None
+    traffic, tsrc = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_intra_latest.json")
     if os.path.exists(pmc):
         with open(pmc) as fh:
             rec = json.load(fh)
-        if rec.get("frames") == F and rec.get("H") == H and rec.get("W") == W:
+        if (rec.get("frames") == F and rec.get("H") == H and rec.get("W") == W
+                and rec.get("libivc_sha256") == lib_sha256()):
             traffic = rec.get("hbm_bytes_per_launch")
-
-    result = {
-        "metric": "Mpixels/s: 4K intra DCT+quant and ±16 full-search ME, 1/2/4/8 MI355X",
+            tsrc = rec.get("source")
+    result.update({
+        "metric": METRIC,
         "value": round(value, 1),
         "unit": "Mpixels/s",
         "n_gpus": world,
@@ -373,148 +382,452 @@ def main():
                    "frames_per_gpu": F, "height": H, "width": W, "parallelism": f"frame-shard x{world}"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": "fused_encode_kernel<u8,f64,C=1>",
+                     "traffic": traffic, "traffic_source": tsrc,
+                     "kernel": "fused_encode_kernel<u8,f64,C=1>",
                      "kernel_ms": round(kern_ms, 4), "algorithmic_bytes_per_launch": algo_bytes,
                      "write_ceiling_GBs": round(fill_gbs, 1),
-                     "store_pace": {"total_GBs": round(pace_rate, 1),
-                                    "late_fraction": round(pace_late, 4),
-                                    "note": "clock-paced address-ordered store sweep, rate "
-                                            "adapted per launch (DESIGN.md §5)"}},
-        "zerorun": {"blocks_per_gpu": nblk, "symbols_per_gpu": nsym,
-                    "ms": round(zms, 3), "Mblocks_per_s": round(nblk / zms / 1e3, 1),
-                    "note": "ZeroRunCoder.encode of the zig-zag output (count, scan, emit kernels)",
-                    "algorithmic_GBs": round((nblk * 256 + nsym * 4) / (zms * 1e-3) / 1e9, 1)},
-        "image2symbols": {"ms": round(fms, 3), "Mpixels_per_s": round(px_step / fms / 1e3, 1),
-                          "same_length_as_two_step": fused_same,
-                          "note": "u8 pixels -> DCT -> quant -> zig-zag -> zero-run symbols fused "
-                                  "(count pass + scan + emit pass; 2 x 1 B/px read, 4 B/symbol "
-                                  "written)",
-                          "algorithmic_GBs": round((px_step + nsym * 4) / (fms * 1e-3) / 1e9, 1)},
-        "exchange": {"alphabet": [b0, b1], "bins": b1 - b0 - 1, "symbols": total_syms,
-                     "entropy_bits_per_symbol": round(entropy_bits(pmf), 4),
-                     "ms": round(exchange_ms, 3),
-                     "collective": f"all_reduce + all_gather_into_tensor ({coll_name(dist)})"
-                     if dist is not None else "none (1 rank)"},
+                     "store_pace": dict(pace, note="clock-paced address-ordered store sweep, "
+                                                   "rate adapted per launch (DESIGN.md §5)")},
+    })
+    return frames, out
+
+
+def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify):
+    import ivclab_amd.device as D
+    from ivclab_amd.distributed import global_bounds, global_histogram
+    from ivclab_amd.entropy.stats import entropy_bits, huffman_bounds, smooth_pmf, stats_marg_from_counts
+    F, H, W = frames.shape[:3]
+    D.intra_encode(frames, table, out, zigzag=True)
+    nblk = out.numel() // 64
+    blocks = out.view(nblk, 64)
+    offs = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
+    probe = torch.empty(1, dtype=torch.int32, device=dev)
+    D.zerorun_encode(blocks, offs, probe)
+    nsym = int(offs[-1].item())
+    sym = torch.empty(nsym, dtype=torch.int32, device=dev)
+    zwall, zms = timed(dist, lambda: D.zerorun_encode(blocks, offs, sym), 3, 1)
+    # the same stream straight from the pixels (fused: the coefficients never reach HBM)
+    sym2 = torch.empty(nsym, dtype=torch.int32, device=dev)
+    nsym_d = torch.zeros(1, dtype=torch.int64, device=dev)
+    fwall, fms = timed(dist, lambda: D.intra_symbols(frames, table, sym2, nsym_d), 3, 1)
+    fused_same = bool(int(nsym_d.item()) == nsym) and bool(torch.equal(sym, sym2))
+    del sym2
+    if verify is not None:
+        from oracle import ivc_oracle as O
+        # frame 0's symbols: its blocks are the first of the stream
+        b0 = H // 8 * (W // 8) * 3
+        n0 = int(offs[b0].item())
+        want = O.zerorun_encode_fast(out[0].cpu().numpy().reshape(-1, 64))
+        check_equal(sym[:n0].cpu().numpy(), np.asarray(want, np.int32), "zerorun frame 0",
+                    verify["failures"])
+        if not fused_same:
+            verify["failures"].append("image2symbols stream != two-step stream")
+        verify["checked"].append("zerorun: frame 0's symbols vs oracle; fused image2symbols "
+                                 "stream == two-step stream (all frames)")
+    mm = torch.empty(2, dtype=torch.int32, device=dev)
+
+    def exchange():
+        D.minmax(sym, mm)
+        lo, hi = global_bounds(mm)
+        b0_, b1_ = huffman_bounds(lo, hi)
+        hist = torch.zeros(b1_ - b0_ - 1, dtype=torch.int64, device=dev)
+        D.histogram(sym, b0_, hist)
+        return b0_, b1_, global_histogram(hist)
+
+    exchange()                      # warm-up: first-launch and allocator costs stay untimed
+    torch.cuda.synchronize()
+    barrier(dist)
+    t_ex = time.perf_counter()
+    b0, b1, ghist = exchange()
+    torch.cuda.synchronize()
+    exchange_ms = (time.perf_counter() - t_ex) * 1e3
+    counts = ghist.cpu().numpy()
+    pmf = smooth_pmf(stats_marg_from_counts(counts))
+    px_step = F * H * W
+    result["zerorun"] = {
+        "blocks_per_gpu": nblk, "symbols_per_gpu": nsym, "ms": round(zms, 3),
+        "Mblocks_per_s": round(nblk / zms / 1e3, 1),
+        "note": "ZeroRunCoder.encode of the zig-zag output (count, scan, emit kernels)",
+        "algorithmic_GBs": round((nblk * 256 + nsym * 4) / (zms * 1e-3) / 1e9, 1)}
+    result["image2symbols"] = {
+        "ms": round(fms, 3), "Mpixels_per_s": round(px_step / fms / 1e3, 1),
+        "same_stream_as_two_step": fused_same,
+        "note": "u8 pixels -> DCT -> quant -> zig-zag -> zero-run symbols fused (count pass + "
+                "scan + emit pass; 2 x 1 B/px read, 4 B/symbol written)",
+        "algorithmic_GBs": round((px_step * 2 + nsym * 4) / (fms * 1e-3) / 1e9, 1)}
+    result["exchange"] = {
+        "alphabet": [b0, b1], "bins": b1 - b0 - 1, "symbols": int(counts.sum()),
+        "entropy_bits_per_symbol": round(entropy_bits(pmf), 4), "ms": round(exchange_ms, 3),
+        "collective": f"all_reduce + all_gather_into_tensor ({coll_name(dist)})"
+        if dist is not None else "none (1 rank)"}
+
+
+def leg_inter(args, dist, rank, world, dev, table, result, verify):
+    import ivclab_amd.device as D
+    Fi, Hi, Wi, sr = args.inter_frames, 1080, 1920, args.sr
+    seq = inter_frames(Fi, Hi, Wi, seed=4 + 1000 * rank, dev=dev)
+    mv = torch.empty((Fi - 1, Hi // 8, Wi // 8), dtype=torch.int64, device=dev)
+    q = torch.empty((Fi - 1, Hi // 8, Wi // 8, 3, 64), dtype=torch.int32, device=dev)
+
+    def istep():
+        D.inter_encode(seq, sr, table, mv, q, zigzag=args.zigzag)
+
+    iwall, ims = timed(dist, istep, args.inter_steps, 1)
+    # the motion search alone (S2 pre-pass + dot4 search kernels, chunked as inside
+    # inter_encode), timed with events on its stream
+    mv2 = torch.empty_like(mv)
+    _, me_ms = timed(None, lambda: D.motion_estimate(seq[:-1], seq[1:], sr, mv2, exact_u8=True),
+                     args.inter_steps, 1)
+    ipx = (Fi - 1) * Hi * Wi
+    cand = valid_candidates(Hi, Wi, sr) * (Fi - 1)
+    dot4 = cand * 16                        # 64 px of c*r per candidate = 16 v_dot4 lane-ops
+    result["inter"] = {
+        "metric": "Mpixels/s: 1080p +-16 full-search ME + MC + residual DCT+quant",
+        "value": round(world * ipx * args.inter_steps / iwall / 1e6, 1), "unit": "Mpixels/s",
+        "ms_per_step": round(iwall / args.inter_steps * 1e3, 3),
+        "config": {"workload": f"cfg4: {Fi} frames 1920x1080 u8 luma per GPU, sr={sr}, "
+                               "ME against the previous source frame (open loop)"},
+        "roofline": {"bound": "valu (v_dot4_u32_u8)", "kernel": "me_s2_kernel + me_fast_u8_kernel<16>",
+                     "kernel_ms": round(me_ms, 4),
+                     "achieved": round(dot4 / (me_ms * 1e-3) / 1e12, 2), "peak": round(DOT4_PEAK_T, 2),
+                     "unit": "T dot4 lane-ops/s", "frac": round(dot4 / (me_ms * 1e-3) / 1e12 / DOT4_PEAK_T, 4),
+                     "useful_dot4_per_launch": dot4,
+                     "note": "useful work = valid candidates x 64 px / 4 (SSD = sum c^2 + S2 - 2X; "
+                             "X by v_dot4_u32_u8, half-rate issue); S2 pre-pass time included"},
     }
+    if verify is not None:
+        torch.cuda.synchronize()
+        from oracle import c_inter_encode
+        host = seq.cpu().numpy()
+        picks = sorted({0, min(32, Fi - 2), Fi - 2})
+        for p in picks:
+            wmv, wq = c_inter_encode(host[p], host[p + 1], sr, 1.0, zigzag=args.zigzag)
+            check_equal(mv[p].cpu().numpy(), wmv[..., 0], f"inter mv pair {p}", verify["failures"])
+            check_equal(q[p].cpu().numpy(), wq.reshape(q.shape[1:]), f"inter q pair {p}",
+                        verify["failures"])
+        check_equal(mv2.cpu().numpy(), mv.cpu().numpy(), "motion_estimate == inter_encode mv",
+                    verify["failures"])
+        verify["checked"].append(f"inter: pairs {picks} of {Fi - 1} whole (mv + q) vs C oracle "
+                                 "chain; motion_estimate leg mv == inter_encode mv (all pairs)")
+    return seq
+
+
+def leg_inter_f64(args, dist, rank, world, dev, seq_u8, result, verify):
+    import ivclab_amd.device as D
+    Fi = min(args.f64_frames, seq_u8.shape[0])
+    sr = args.sr
+    y = luma_f64(seq_u8[:Fi]).contiguous()
+    _, Hi, Wi = y.shape
+    mv = torch.empty((Fi - 1, Hi // 8, Wi // 8), dtype=torch.int64, device=dev)
+
+    def step():
+        D.motion_estimate(y[:-1], y[1:], sr, mv)
+
+    wall, ms = timed(dist, step, args.inter_steps, 1)
+    cand = valid_candidates(Hi, Wi, sr) * (Fi - 1)
+    ops = cand * 64 * 3                     # sub, mul, add per candidate-pixel (no FMA)
+    result["inter_f64"] = {
+        "metric": "Mpixels/s: 1080p +-16 full-search ME, NumPy-semantics float64 SSD",
+        "value": round(world * (Fi - 1) * Hi * Wi * args.inter_steps / wall / 1e6, 1),
+        "unit": "Mpixels/s", "ms_per_step": round(wall / args.inter_steps * 1e3, 3),
+        "config": {"workload": f"{Fi} frames 1920x1080 non-integer float64 luma per GPU, sr={sr}, "
+                               "MotionCompensator.compute_motion_vector semantics (pairwise "
+                               "np.sum order, first strict minimum)"},
+        "roofline": {"bound": "valu (fp64)", "kernel": "me_f64 search", "kernel_ms": round(ms, 4),
+                     "achieved": round(ops / (ms * 1e-3) / 1e12, 2), "peak": F64_PEAK_T,
+                     "unit": "T fp64 op/s", "frac": round(ops / (ms * 1e-3) / 1e12 / F64_PEAK_T, 4),
+                     "algorithmic_ops_per_launch": ops,
+                     "note": "3 ops (sub, mul, add) per valid candidate-pixel; peak = FP64 "
+                             "vector 78.6 TFLOPS / 2 (no FMA: NumPy rounds d*d)"},
+    }
+    if verify is not None:
+        torch.cuda.synchronize()
+        from oracle import c_motion_vectors
+        p = Fi // 2
+        yh = y[p:p + 2].cpu().numpy()
+        check_equal(mv[p].cpu().numpy(), c_motion_vectors(yh[0], yh[1], sr)[..., 0],
+                    f"f64 ME pair {p}", verify["failures"])
+        verify["checked"].append(f"inter_f64: pair {p} whole vs C oracle (NumPy pairwise SSD)")
+
+
+def leg_class_api(args, dev, result, verify):
+    """Host arrays through the drop-in classes (each call stages H2D, runs its kernel and
+    copies back, as a NumPy caller sees it) and through the one-call host entry point."""
+    from ivclab_amd import DiscreteCosineTransform, Patcher, PatchQuant, ZigZag
+    from ivclab_amd import _native as N
+    dct, pq, zz, pt = DiscreteCosineTransform(), PatchQuant(1.0), ZigZag(), Patcher()
+    t = N.table_arg(pq.get_quantization_table())
+    rng = np.random.default_rng(1)
+    cases = {
+        "4k_luma": intra_frames(1, 2160, 3840, seed=3, dev=dev)[0].cpu().numpy()[..., None],
+        "cfg2_1080p_rgb": rng.integers(0, 256, (1080, 1920, 3), dtype=np.uint8),
+    }
+    out = {}
+    for name, img in cases.items():
+        H, W, C = img.shape
+
+        def classes():
+            return zz.flatten(pq.quantize(dct.transform(pt.patch(img))))
+
+        def one_call():
+            o = np.empty((1, H // 8, W // 8, 3, 64), np.int32)
+            N.check(N.lib().ivc_intra_encode(N.ptr(np.ascontiguousarray(img[None])), 1, 1, H, W, C,
+                                             N.ptr(t), N.F64, 1, N.ptr(o)))
+            return o
+
+        res = {}
+        for label, fn, reps in (("classes", classes, 3), ("one_call", one_call, 5)):
+            fn()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                r = fn()
+            dt = (time.perf_counter() - t0) / reps
+            res[label] = {"ms": round(dt * 1e3, 3), "Mpixels_per_s": round(H * W / dt / 1e6, 1)}
+            if verify is not None:
+                from oracle import ivc_oracle as O
+                want = O.intra_encode(img, 1.0, zigzag=True)
+                check_equal(np.asarray(r).reshape(want.shape), want, f"class_api {name} {label}",
+                            verify["failures"])
+        res["shape"] = list(img.shape)
+        out[name] = res
+    if verify is not None:
+        verify["checked"].append("class_api: every timed output vs oracle")
+    result["class_api"] = dict(out, note="host NumPy in -> host NumPy out, PCIe included "
+                                         "(DCT.transform -> PatchQuant.quantize -> ZigZag.flatten "
+                                         "as separate calls, or the fused ivc_intra_encode); "
+                                         "not comparable with the device-resident `value`")
+
+
+def make_sharded_step(D, N, seq, pairs, sr, table, mv, q, hist, chunk, hist_wg, zigzag, side):
+    """The cfg5 step: ME + MC + residual DCT + quantise of this rank's pairs, then the symbol
+    histograms (coefficients | MV indices).  The pairs go in chunks of `chunk`: ME is
+    VALU-bound and the histogram HBM-bound, so chunk k's histograms run on a side stream
+    (at `hist_wg` workgroups per CU) while chunk k+1 is encoded (same work, same counts:
+    integer adds).  Returns the local histogram (the caller all-gathers it)."""
+    def step():
+        main = torch.cuda.current_stream()
+        L = N.lib()
+        prev_wg = L.ivc_histogram_occupancy()
+        N.check(L.ivc_set_histogram_occupancy(hist_wg))
+        try:
+            hist.zero_()
+            for p0 in range(0, pairs, chunk):
+                p1 = min(p0 + chunk, pairs)
+                D.inter_encode(seq[p0:p1 + 1], sr, table, mv[p0:p1], q[p0:p1], zigzag=zigzag,
+                               stream=main)
+                side.wait_stream(main)
+                D.histogram(q[p0:p1].view(-1), HIST_LO, hist[:HIST_BINS], stream=side)
+                D.histogram(mv[p0:p1].view(-1), 0, hist[HIST_BINS:], stream=side)
+            main.wait_stream(side)
+        finally:
+            N.check(L.ivc_set_histogram_occupancy(prev_wg))
+        return hist
+    return step
+
+
+def leg_sharded(args, dist, rank, world, dev, table, result, verify):
+    import ivclab_amd.device as D
+    from ivclab_amd import _native as N
+    from ivclab_amd.distributed import global_histogram, shard_pairs
+    F5, H5, W5, sr5 = args.sharded_frames, args.sharded_height, args.sharded_width, 16
+    a5, b5 = shard_pairs(F5, rank, world)          # this rank's frames incl. the halo
+    n5 = max(b5 - a5, 0)
+    seq5 = inter_frames(max(n5, 2), H5, W5, seed=5, dev=dev, first=a5)[:n5]
+    pairs5 = max(n5 - 1, 0)
+    mv5 = torch.empty((max(pairs5, 1), H5 // 8, W5 // 8), dtype=torch.int64, device=dev)
+    q5 = torch.empty((max(pairs5, 1), H5 // 8, W5 // 8, 3, 64), dtype=torch.int32, device=dev)
+    nmv = (2 * sr5 + 1) ** 2
+    hist5 = torch.zeros(HIST_BINS + nmv, dtype=torch.int64, device=dev)
+    side = torch.cuda.Stream(device=dev)
+    ck = args.sharded_chunk if args.sharded_chunk > 0 else max(pairs5, 1)
+    local = make_sharded_step(D, N, seq5, pairs5, sr5, table, mv5, q5, hist5, ck,
+                              args.sharded_hist_wg, args.zigzag, side)
+
+    def sstep():
+        return global_histogram(local())
+
+    swall, _ = timed(dist, sstep, args.sharded_steps, 1)
+    g5 = sstep()
+    torch.cuda.synchronize()
+    g5h = g5.cpu().numpy()
+    total5 = (F5 - 1) * H5 * W5
+    result["sharded"] = {
+        "metric": "Mpixels/s: 8K frame-sharded +-16 ME + residual DCT+quant with one "
+                  "histogram all-gather (cfg5)",
+        "value": round(total5 * args.sharded_steps / swall / 1e6, 1), "unit": "Mpixels/s",
+        "scaling": "strong",
+        "ms_per_step": round(swall / args.sharded_steps * 1e3, 3),
+        "config": {"workload": f"cfg5: {F5} frames {W5}x{H5} u8 luma split across {world} "
+                               f"rank(s) (+1 halo frame each), sr={sr5}",
+                   "pairs_per_rank_max": int(max_over_ranks(dist, float(pairs5)))},
+        "exchange": {"collective": f"all_gather_into_tensor ({coll_name(dist)})"
+                     if dist is not None else "none (1 rank)",
+                     "bins": HIST_BINS + nmv,
+                     "symbols": int(g5h[:HIST_BINS].sum()),
+                     "motion_vectors": int(g5h[HIST_BINS:].sum()),
+                     "hist_checksum": int((g5h * np.arange(1, g5h.size + 1, dtype=np.int64)).sum()),
+                     "hist_sha256": hashlib.sha256(g5h.tobytes()).hexdigest()[:16]},
+        "chunk_pairs": ck,
+    }
+    if verify is not None and pairs5 > 0:
+        from oracle import c_inter_encode
+        h5 = H5 // 8
+        stripes = ((0, 3), (h5 // 2 - 1, h5 // 2 + 2), (h5 - 3, h5))
+        for p in sorted({0, pairs5 - 1}):
+            host = seq5[p:p + 2].cpu().numpy()
+            for rows in stripes:
+                wmv, wq = c_inter_encode(host[0], host[1], sr5, 1.0, zigzag=args.zigzag, rows=rows)
+                check_equal(mv5[p, rows[0]:rows[1]].cpu().numpy(), wmv[..., 0],
+                            f"sharded rank {rank} pair {a5 + p} mv rows {rows}", verify["failures"])
+                check_equal(q5[p, rows[0]:rows[1]].cpu().numpy(), wq.reshape((rows[1] - rows[0],) + q5.shape[2:]),
+                            f"sharded rank {rank} pair {a5 + p} q rows {rows}", verify["failures"])
+        verify["checked"].append(f"sharded: rank {rank}'s first and last pair, 3 block-row "
+                                 "stripes each, mv + q vs C oracle chain")
+    del seq5, mv5, q5
+    torch.cuda.empty_cache()
+    if verify is not None:
+        # the whole sequence on rank 0 alone, one unchunked inter_encode call and main-stream
+        # histograms: the gathered histogram must be identical
+        if rank == 0:
+            full = inter_frames(F5, H5, W5, seed=5, dev=dev)
+            mvf = torch.empty((F5 - 1, H5 // 8, W5 // 8), dtype=torch.int64, device=dev)
+            qf = torch.empty((F5 - 1, H5 // 8, W5 // 8, 3, 64), dtype=torch.int32, device=dev)
+            D.inter_encode(full, sr5, table, mvf, qf, zigzag=args.zigzag)
+            hf = torch.zeros(HIST_BINS + nmv, dtype=torch.int64, device=dev)
+            D.histogram(qf.view(-1), HIST_LO, hf[:HIST_BINS])
+            D.histogram(mvf.view(-1), 0, hf[HIST_BINS:])
+            torch.cuda.synchronize()
+            check_equal(g5h, hf.cpu().numpy(), "sharded histogram vs 1-rank unchunked run",
+                        verify["failures"])
+            verify["checked"].append(f"sharded: gathered histogram of {world} rank(s) == one "
+                                     "unsharded, unchunked run on rank 0")
+            del full, mvf, qf, hf
+            torch.cuda.empty_cache()
+        barrier(dist)
+
+
+# ---------------------------------------------------------------- main ------------------
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=6)
+    ap.add_argument("--frames", type=int, default=256)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--inter-frames", type=int, default=300)
+    ap.add_argument("--inter-steps", type=int, default=3)
+    ap.add_argument("--f64-frames", type=int, default=60,
+                    help="frames of the float64 ME leg (a prefix of the cfg4 sequence)")
+    ap.add_argument("--sr", type=int, default=16)
+    ap.add_argument("--zigzag", action="store_true")
+    ap.add_argument("--no-inter", action="store_true")
+    ap.add_argument("--no-intra", action="store_true", help="profiling aid: skip the cfg3 leg")
+    ap.add_argument("--no-symbols", action="store_true", help="skip the zero-run/exchange legs")
+    ap.add_argument("--no-f64", action="store_true", help="skip the float64 ME leg")
+    ap.add_argument("--no-class-api", action="store_true", help="skip the host-buffer leg")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the cfg5 8K leg")
+    ap.add_argument("--no-cpu-pool", action="store_true", help="skip the multi-core CPU leg")
+    ap.add_argument("--no-verify", action="store_true", help="skip the oracle checks")
+    ap.add_argument("--sharded-frames", type=int, default=120)
+    ap.add_argument("--sharded-height", type=int, default=4320)
+    ap.add_argument("--sharded-width", type=int, default=7680)
+    ap.add_argument("--sharded-steps", type=int, default=3)
+    ap.add_argument("--sharded-hist-wg", type=int, default=2,
+                    help="workgroups per CU of the side-stream histograms in the cfg5 step (0-16)")
+    ap.add_argument("--sharded-chunk", type=int, default=8,
+                    help="frame pairs per inter_encode call in the cfg5 step; the histogram of "
+                         "chunk k runs on a side stream while chunk k+1 is encoded (0: one call)")
+    args = ap.parse_args(argv)
+    if not 0 <= args.sharded_hist_wg <= 16:
+        ap.error("--sharded-hist-wg must be in [0, 16]")
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    return args
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # start the ranks ourselves (nothing has touched the GPU yet) and pass their status on
+        sys.exit(subprocess.call(launcher_cmd(args.gpus, sys.argv[1:], free_port())))
+    dist, rank, world, local = dist_setup(args.gpus)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    from ivclab_amd import PatchQuant
+    table = PatchQuant(1.0).get_quantization_table()
+    verify = None if args.no_verify else {"checked": [], "failures": []}
+    result = {}
+    t_start = time.perf_counter()
+
+    # ---- cfg3: 4K intra DCT + quant (the headline) ----------------------------------------
+    if args.no_intra:
+        args.frames = 1
+    frames, out = leg_intra(args, dist, rank, world, dev, table, result, verify)
+    if not args.no_symbols:
+        leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify)
     del out, frames
     torch.cuda.empty_cache()
 
     # ---- cfg4: 1080p x 300, +-16 ME + MC + residual DCT + quant ------------------------------
     if not args.no_inter:
-        Fi, Hi, Wi, sr = args.inter_frames, 1080, 1920, args.sr
-        seq = inter_frames(Fi, Hi, Wi, seed=4 + 1000 * rank, dev=dev)
-        mv = torch.empty((Fi - 1, Hi // 8, Wi // 8), dtype=torch.int64, device=dev)
-        q = torch.empty((Fi - 1, Hi // 8, Wi // 8, 3, 64), dtype=torch.int32, device=dev)
-
-        def istep():
-            D.inter_encode(seq, sr, table, mv, q, zigzag=args.zigzag)
-
-        iwall, ims = timed(dist, istep, args.inter_steps, 1)
-        ipx = (Fi - 1) * Hi * Wi
-        ivalue = world * ipx * args.inter_steps / iwall / 1e6
-        result["inter"] = {
-            "metric": "Mpixels/s: 1080p +-16 full-search ME + MC + residual DCT+quant",
-            "value": round(ivalue, 1), "unit": "Mpixels/s",
-            "ms_per_step": round(iwall / args.inter_steps * 1e3, 3),
-            "config": {"workload": f"cfg4: {Fi} frames 1920x1080 u8 luma per GPU, sr={sr}, "
-                                   "ME against the previous source frame (open loop)"},
-        }
+        seq = leg_inter(args, dist, rank, world, dev, table, result, verify)
+        if not args.no_f64:
+            leg_inter_f64(args, dist, rank, world, dev, seq, result, verify)
         if rank == 0 and not args.no_cpu:
-            host = seq[:2].cpu().numpy()
-            mpx, per_cand, _ = cpu_baseline_me(host, sr)
+            mpx, per_cand = cpu_baseline_me(seq[:2].cpu().numpy(), args.sr)
             result["inter"]["cpu_baseline"] = {
                 "value": round(mpx, 4), "unit": "Mpixels/s", "cores": 1, "kind": "port",
-                "sample": f"reference ME loop (oracle motion_vectors_loop, float64) on 2 block rows "
-                          f"of a 1080p pair at sr={sr}; {per_cand * 1e6:.3f} us per valid candidate, "
-                          "extrapolated by exact valid-candidate count"}
-        del seq, mv, q
+                "sample": f"reference ME loop (oracle motion_vectors_loop, float64) on 4 block rows "
+                          f"of a 1080p pair at sr={args.sr}; {per_cand * 1e6:.3f} us per valid "
+                          "candidate, extrapolated by exact valid-candidate count"}
+        del seq
         torch.cuda.empty_cache()
+
+    # ---- host buffers through the classes (PCIe included) ---------------------------------
+    if rank == 0 and not args.no_class_api:
+        leg_class_api(args, dev, result, verify)
 
     # ---- cfg5: 8K x 120 frames, frame-sharded ME + DCT, one all-gather of histograms ------
     if not args.no_sharded:
-        from ivclab_amd.distributed import shard_pairs
-        from ivclab_amd import _native as N
-        F5, H5, W5, sr5 = args.sharded_frames, 4320, 7680, 16
-        a5, b5 = shard_pairs(F5, rank, world)          # this rank's frames incl. the halo
-        n5 = max(b5 - a5, 0)
-        seq5 = inter_frames(max(n5, 2), H5, W5, seed=5, dev=dev, first=a5)[:n5]
-        pairs5 = max(n5 - 1, 0)
-        mv5 = torch.empty((max(pairs5, 1), H5 // 8, W5 // 8), dtype=torch.int64, device=dev)
-        q5 = torch.empty((max(pairs5, 1), H5 // 8, W5 // 8, 3, 64), dtype=torch.int32, device=dev)
-        nmv = (2 * sr5 + 1) ** 2
-        hist5 = torch.zeros(HIST_BINS + nmv, dtype=torch.int64, device=dev)
-
-        side = torch.cuda.Stream(device=dev)
-        ck = args.sharded_chunk if args.sharded_chunk > 0 else max(pairs5, 1)
-
-        def sstep():
-            # the step: ME + MC + residual DCT + quantise of this rank's pairs, then the
-            # symbol histograms (coefficients | MV indices) and their all-gather.  The pairs
-            # go in chunks of `ck`: ME is VALU-bound and the histogram HBM-bound, so chunk k's
-            # histograms run on a side stream while chunk k+1 is encoded (same work, same
-            # counts: integer adds in one stream order)
-            main = torch.cuda.current_stream()
-            L = N.lib()
-            prev_wg = L.ivc_histogram_occupancy()
-            N.check(L.ivc_set_histogram_occupancy(args.sharded_hist_wg))
-            hist5.zero_()
-            for p0 in range(0, pairs5, ck):
-                p1 = min(p0 + ck, pairs5)
-                D.inter_encode(seq5[p0:p1 + 1], sr5, table, mv5[p0:p1], q5[p0:p1],
-                               zigzag=args.zigzag, stream=main)
-                side.wait_stream(main)
-                D.histogram(q5[p0:p1].view(-1), HIST_LO, hist5[:HIST_BINS], stream=side)
-                D.histogram(mv5[p0:p1].view(-1), 0, hist5[HIST_BINS:], stream=side)
-            main.wait_stream(side)
-            N.check(L.ivc_set_histogram_occupancy(prev_wg))
-            return global_histogram(hist5)
-
-        swall, _ = timed(dist, sstep, args.sharded_steps, 1)
-        g5 = sstep()
-        total5 = (F5 - 1) * H5 * W5
-        result["sharded"] = {
-            "metric": "Mpixels/s: 8K frame-sharded +-16 ME + residual DCT+quant with one "
-                      "histogram all-gather (cfg5)",
-            "value": round(total5 * args.sharded_steps / swall / 1e6, 1), "unit": "Mpixels/s",
-            "scaling": "strong",
-            "ms_per_step": round(swall / args.sharded_steps * 1e3, 3),
-            "config": {"workload": f"cfg5: {F5} frames {W5}x{H5} u8 luma split across {world} "
-                                   f"rank(s) (+1 halo frame each), sr={sr5}",
-                       "pairs_per_rank_max": int(max_over_ranks(dist, float(pairs5)))},
-            "exchange": {"collective": f"all_gather_into_tensor ({coll_name(dist)})"
-                         if dist is not None else "none (1 rank)",
-                         "bins": HIST_BINS + nmv,
-                         "symbols": int(g5[:HIST_BINS].sum().item()),
-                         "motion_vectors": int(g5[HIST_BINS:].sum().item()),
-                         "hist_checksum": int((g5 * torch.arange(1, g5.numel() + 1, device=dev))
-                                              .sum().item())},
-            "chunk_pairs": ck,
-        }
-        del seq5, mv5, q5
-        torch.cuda.empty_cache()
+        leg_sharded(args, dist, rank, world, dev, table, result, verify)
 
     if rank == 0 and not args.no_cpu:
-        host = intra_frames(80, H, W, seed=3, dev=dev).cpu().numpy()
+        host = intra_frames(80, args.height, args.width, seed=3, dev=dev).cpu().numpy()
         mpx, n, dt = cpu_baseline_intra(host)
         result["cpu_baseline"] = {
             "value": round(mpx, 3), "unit": "Mpixels/s", "cores": 1, "kind": "port",
             "sample": f"oracle (scipy dct + np.round quantise, the reference's algorithm) on {n} "
-                      f"whole {W}x{H} frames of the same generator, {dt:.1f} s single-threaded",
+                      f"whole {args.width}x{args.height} frames of the same generator, {dt:.1f} s "
+                      "single-threaded",
             "cpu": cpu_model()}
         if not args.no_cpu_pool:
             pair = inter_frames(2, 1080, 1920, seed=4, dev=dev).cpu().numpy()
-            impx, mmpx, P = cpu_baseline_pool(host[:16], pair, args.sr)
+            impx, mmpx, P, share = cpu_baseline_pool(host[:16], pair, args.sr)
             result["cpu_baseline_multicore"] = {
                 "intra_value": round(impx, 3), "me_value": round(mmpx, 4), "unit": "Mpixels/s",
-                "cores": P, "kind": "port", "cpu": cpu_model(),
-                "sample": f"the same oracle paths frame-sharded over {P} worker processes: intra "
-                          "on whole 4K frames (~4 s), the ME loop on one 16-row stripe of a "
-                          "1080p pair per worker, extrapolated per valid candidate"}
+                "cores": P, "kind": "port", "cpu": cpu_model(), "share": share,
+                "sample": f"the same oracle paths frame-sharded over {P} worker processes (every "
+                          "core the box grants: affinity, capped by the cgroup quota): intra on "
+                          "whole 4K frames (~4 s), the ME loop on one 16-row stripe of a 1080p "
+                          "pair per worker, extrapolated per valid candidate"}
 
+    if verify is not None:
+        fails = verify["failures"]
+        if dist is not None:
+            nf = max_over_ranks(dist, float(len(fails)))
+            fails_all = int(nf)
+        else:
+            fails_all = len(fails)
+        result["verify"] = {"ok": fails_all == 0, "failures_rank0": fails,
+                            "checked_rank0": verify["checked"]}
+    result["bench_wall_s"] = round(time.perf_counter() - t_start, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+    if verify is not None and result["verify"]["ok"] is False:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

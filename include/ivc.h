@@ -183,7 +183,8 @@ int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbi
  * the default).  A histogram on a side stream next to a VALU-bound kernel (the frame-sharded
  * bench step overlaps chunk k's histogram with chunk k+1's motion search) runs better with
  * 1-2, leaving LDS and wave slots to the other stream.  Timing only: counts are identical.
- * No reference counterpart.                                                               */
+ * The setting is process-wide: it applies to every device, thread and histogram launch
+ * (including intra_encode's fused histogram) until set again.  No reference counterpart.  */
 int ivc_set_histogram_occupancy(int wg_per_cu);
 int ivc_histogram_occupancy(void);
 

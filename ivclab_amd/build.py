@@ -36,12 +36,7 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(d) <= t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [hipcc()] + FLAGS + ["-o", tmp] + [os.path.join(CSRC, f) for f in SOURCES]
+def _run(cmd, verbose):
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -49,6 +44,25 @@ def build(force: bool = False, verbose: bool = False) -> str:
         raise RuntimeError(f"hipcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
     if verbose and r.stderr.strip():
         print(r.stderr, file=sys.stderr)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    """Compile each translation unit to an object (in parallel, under ivclab_amd/_lib/obj),
+    then link the shared library."""
+    if not force and up_to_date():
+        return OUT
+    from concurrent.futures import ThreadPoolExecutor
+    objdir = os.path.join(os.path.dirname(OUT), "obj")
+    os.makedirs(objdir, exist_ok=True)
+    compile_flags = [f for f in FLAGS if f != "-shared"]
+    objs = [os.path.join(objdir, os.path.splitext(f)[0] + ".o") for f in SOURCES]
+    jobs = [[hipcc()] + compile_flags + ["-c", "-o", o, os.path.join(CSRC, f)]
+            for f, o in zip(SOURCES, objs)]
+    workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0") or 0) or os.cpu_count() or 1))
+    with ThreadPoolExecutor(workers) as ex:
+        list(ex.map(lambda c: _run(c, verbose), jobs))
+    tmp = OUT + ".tmp"
+    _run([hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs, verbose)
     os.replace(tmp, OUT)
     return OUT
 

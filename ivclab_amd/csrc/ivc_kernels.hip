@@ -13,6 +13,7 @@
 // workgroup writes its contiguous output span with 16-byte stores.  HBM traffic per unit
 // is one read of the input and one write of the output.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <mutex>
 #include <unordered_map>
@@ -1350,7 +1351,8 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
 #pragma unroll
   for (int k = 0; k < HIST_HOT_N; ++k) hot[k] = 0;
   auto count = [&](S v) {
-    const uint64_t u = (uint64_t)((int64_t)v - (int64_t)HIST_HOT_LO);
+    // unsigned difference: v - HIST_HOT_LO wraps instead of overflowing for v near INT64_MAX
+    const uint64_t u = (uint64_t)(int64_t)v - (uint64_t)(int64_t)HIST_HOT_LO;
     if (u < (uint64_t)HIST_HOT_N) {
 #pragma unroll
       for (int k = 0; k < HIST_HOT_N; ++k) hot[k] += u == (uint64_t)k ? 1u : 0u;
@@ -1412,10 +1414,12 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
 }
 
 // workgroups per CU of the histogram launches: 4 fills the chip (the stream alone is
-// HBM-bound); fewer leave LDS and wave slots to kernels on other streams
-static int g_hist_wg_per_cu = 4;
-int histogram_wg_per_cu() { return g_hist_wg_per_cu; }
-void set_histogram_wg_per_cu(int k) { g_hist_wg_per_cu = k > 0 ? k : 4; }
+// HBM-bound); fewer leave LDS and wave slots to kernels on other streams.  Process-wide
+// (every device, every thread, every histogram launch incl. intra_encode's fused one);
+// atomic so a set on one thread never races a launch reading it on another
+static std::atomic<int> g_hist_wg_per_cu{4};
+int histogram_wg_per_cu() { return g_hist_wg_per_cu.load(std::memory_order_relaxed); }
+void set_histogram_wg_per_cu(int k) { g_hist_wg_per_cu.store(k > 0 ? k : 4, std::memory_order_relaxed); }
 
 template <typename S>
 static hipError_t launch_hist(const S* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist,
@@ -1423,7 +1427,7 @@ static hipError_t launch_hist(const S* sym, int64_t n, int64_t lo, int32_t nbins
   if (n <= 0 || nbins <= 0) return hipSuccess;
   const int use_lds = nbins <= 16384;
   const size_t lds = use_lds ? (size_t)nbins * 4 : 0;
-  histogram_kernel<S><<<grid_for(n, 256 * 16, g_hist_wg_per_cu), 256, lds, s>>>(
+  histogram_kernel<S><<<grid_for(n, 256 * 16, histogram_wg_per_cu()), 256, lds, s>>>(
       sym, n, lo, nbins, reinterpret_cast<unsigned long long*>(hist), use_lds);
   return hipGetLastError();
 }

@@ -1,0 +1,145 @@
+"""Parity of the exact chains bench.py times, at (or past) their workload sizes.
+
+bench.py's legs run code paths the small parity tests never reach: the fast exact-u8 motion
+search over many frame pairs in 256 MB S2 chunks (32 pairs per chunk at 1080p) feeding the
+SRC_INTER residual DCT + quantiser (cfg4), the fused intra kernel writing a batch whose
+output lies past 4 GiB (cfg3), and the chunked cfg5 step with its side-stream histograms.
+These tests run those chains on the bench's own synthetic generators and compare sampled
+frames (whole frames, every block) with the C/NumPy oracle (oracle.c_inter_encode:
+motion.py:8-97 + videocodec.py:52-73 + dct.py:12-28 + patchquant.py:44-60)."""
+import numpy as np
+import pytest
+
+from oracle import c_inter_encode
+from oracle import ivc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+import bench  # noqa: E402  (the bench's own synthetic generators)
+import ivclab_amd.device as D  # noqa: E402
+from ivclab_amd import PatchQuant  # noqa: E402
+
+TABLE = PatchQuant(1.0).get_quantization_table()
+
+
+def assert_bits(a, b, what=""):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.dtype == b.dtype, f"{what}: dtype {a.dtype} != {b.dtype}"
+    assert a.shape == b.shape, f"{what}: shape {a.shape} != {b.shape}"
+    if a.tobytes() != b.tobytes():
+        bad = np.flatnonzero(a.reshape(-1) != b.reshape(-1))
+        raise AssertionError(f"{what}: {bad.size} differing elements, first at {bad[0]}")
+
+
+def test_inter_encode_sr16_1080p_across_s2_chunks():
+    """cfg4's chain at its frame size: 40 frames of the bench's 1080p sequence at sr = 16
+    (the fast dot4 search; 39 pairs = two S2 chunks of 32 + 7).  Pairs 0, 31 (last of chunk
+    0), 32 (first of chunk 1) and 38 (last) are checked whole — every motion vector and every
+    quantised residual coefficient — against the C oracle chain."""
+    dev = torch.device("cuda:0")
+    F, H, W, sr = 40, 1080, 1920, 16
+    seq = bench.inter_frames(F, H, W, seed=4, dev=dev)
+    mv = torch.full((F - 1, H // 8, W // 8), -1, dtype=torch.int64, device=dev)
+    q = torch.full((F - 1, H // 8, W // 8, 3, 64), -7, dtype=torch.int32, device=dev)
+    D.inter_encode(seq, sr, TABLE, mv, q)
+    torch.cuda.synchronize()
+    host = seq.cpu().numpy()
+    for p in (0, 31, 32, F - 2):
+        wmv, wq = c_inter_encode(host[p], host[p + 1], sr, 1.0)
+        assert_bits(mv[p].cpu().numpy(), wmv[..., 0], f"mv pair {p}")
+        assert_bits(q[p].cpu().numpy(), wq.reshape(H // 8, W // 8, 3, 64), f"q pair {p}")
+    # every pair was written (no chunk skipped): indices in range, no sentinel left
+    m = mv.cpu().numpy()
+    assert m.min() >= 0 and m.max() < (2 * sr + 1) ** 2
+
+
+def test_inter_encode_sr16_zigzag_and_motion_range():
+    """The zig-zag variant of the same chain on a sequence whose motion spans the whole
+    +-16 window (large shifts, flat and textured regions), 4 pairs checked whole."""
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(416)
+    H, W, sr = 272, 480, 16
+    lo = rng.integers(0, 256, (H // 4 + 12, W // 4 + 12)).astype(np.float64)
+    base = np.kron(lo, np.ones((4, 4))) + rng.integers(-3, 4, (H + 48, W + 48))
+    base = np.clip(base, 0, 255).astype(np.uint8)
+    shifts = [(0, 0), (16, -16), (-16, 16), (7, -13), (0, 0)]
+    frames = np.stack([base[24 + dy:24 + dy + H, 24 + dx:24 + dx + W] for dy, dx in shifts])
+    frames[2, 40:120, 100:300] = 90                               # flat: tie-break path
+    F = len(frames)
+    seq = torch.from_numpy(np.ascontiguousarray(frames)).to(dev)
+    mv = torch.empty((F - 1, H // 8, W // 8), dtype=torch.int64, device=dev)
+    q = torch.empty((F - 1, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+    D.inter_encode(seq, sr, TABLE, mv, q, zigzag=True)
+    torch.cuda.synchronize()
+    for p in range(F - 1):
+        wmv, wq = c_inter_encode(frames[p], frames[p + 1], sr, 1.0, zigzag=True)
+        assert_bits(mv[p].cpu().numpy(), wmv[..., 0], f"mv pair {p}")
+        assert_bits(q[p].cpu().numpy(), wq, f"q pair {p}")
+
+
+def test_intra_encode_batch_past_4gib():
+    """cfg3's kernel on 48 4K frames of the bench generator: the int32 output is 4.78 GB, so
+    the buffer-descriptor rebase has to carry offsets past 4 GiB.  Frames 0, 23, 24 and 47
+    (first, either side of the middle, last: the last lies entirely beyond 4 GiB) are checked
+    whole against the oracle; the rest are checked to have been written."""
+    dev = torch.device("cuda:0")
+    F, H, W = 48, 2160, 3840
+    frames = bench.intra_frames(F, H, W, seed=3, dev=dev).view(F, H, W, 1)
+    out = torch.full((F, H // 8, W // 8, 3, 64), -(1 << 30), dtype=torch.int32, device=dev)
+    assert out.numel() * 4 > (1 << 32) + H // 8 * W // 8 * 3 * 64 * 4
+    D.intra_encode(frames, TABLE, out)
+    torch.cuda.synchronize()
+    for f in (0, 23, 24, F - 1):
+        want = O.intra_encode(frames[f].cpu().numpy(), 1.0).reshape(H // 8, W // 8, 3, 64)
+        assert_bits(out[f].cpu().numpy(), want, f"frame {f}")
+    # the sentinel is outside every quantised value's range: nothing left unwritten
+    assert int((out == -(1 << 30)).sum().item()) == 0
+
+
+def test_chunked_inter_encode_with_side_stream_histograms():
+    """The cfg5 step shape: inter_encode in chunks of 2 pairs with each chunk's coefficient
+    and motion-vector histograms on a side stream while the next chunk is encoded, at reduced
+    histogram occupancy, gives the same mv, q and histograms as one call followed by the
+    histograms on the main stream."""
+    import ivclab_amd._native as N
+    dev = torch.device("cuda:0")
+    F, H, W, sr = 7, 1080, 1920, 16
+    seq = bench.inter_frames(F, H, W, seed=5, dev=dev)
+    P = F - 1
+    nmv = (2 * sr + 1) ** 2
+
+    def run(chunk, wg):
+        mv = torch.empty((P, H // 8, W // 8), dtype=torch.int64, device=dev)
+        q = torch.empty((P, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+        hist = torch.zeros(bench.HIST_BINS + nmv, dtype=torch.int64, device=dev)
+        main, side = torch.cuda.current_stream(), torch.cuda.Stream(device=dev)
+        L = N.lib()
+        prev = L.ivc_histogram_occupancy()
+        N.check(L.ivc_set_histogram_occupancy(wg))
+        try:
+            for p0 in range(0, P, chunk):
+                p1 = min(p0 + chunk, P)
+                D.inter_encode(seq[p0:p1 + 1], sr, TABLE, mv[p0:p1], q[p0:p1], stream=main)
+                side.wait_stream(main)
+                D.histogram(q[p0:p1].view(-1), bench.HIST_LO, hist[:bench.HIST_BINS], stream=side)
+                D.histogram(mv[p0:p1].view(-1), 0, hist[bench.HIST_BINS:], stream=side)
+            main.wait_stream(side)
+            torch.cuda.synchronize()
+        finally:
+            N.check(L.ivc_set_histogram_occupancy(prev))
+        return mv.cpu().numpy(), q.cpu().numpy(), hist.cpu().numpy()
+
+    mv1, q1, h1 = run(P, 0)
+    mv2, q2, h2 = run(2, 2)
+    assert_bits(mv2, mv1, "mv chunked")
+    assert_bits(q2, q1, "q chunked")
+    assert_bits(h2, h1, "hist chunked")
+    assert h1[:bench.HIST_BINS].sum() == q1.size and h1[bench.HIST_BINS:].sum() == mv1.size
+    assert np.array_equal(h1[bench.HIST_BINS:], O.histogram(mv1, 0, nmv))
+    assert np.array_equal(h1[:bench.HIST_BINS], O.histogram(q1, bench.HIST_LO, bench.HIST_BINS))
+    # and pair 3 of the chunked run against the oracle
+    host = seq.cpu().numpy()
+    wmv, wq = c_inter_encode(host[3], host[4], sr, 1.0)
+    assert_bits(mv2[3], wmv[..., 0], "mv pair 3")
+    assert_bits(q2[3], wq.reshape(H // 8, W // 8, 3, 64), "q pair 3")
