@@ -70,6 +70,14 @@ int ivc_release_scratch(void);
 int ivc_set_store_pace(double total_gbps);
 double ivc_store_pace(void);
 double ivc_store_pace_late(void);
+/* Measurement statistics of the current device's paced launches since the last reset
+ * (encoder 0 = image source, 1 = inter residual), folding every completed launch first:
+ * out[0] launches measured, [1] launches over the late threshold, [2] mean and [3] maximum
+ * late fraction, [4] current rate (GB/s), [5] last late fraction, [6] mean achieved GB/s of
+ * the measured launches (bytes / event time), [7] measurements still in flight.  Writes
+ * min(n, 8) values and returns that count (a negative status on a bad argument).          */
+int ivc_store_pace_stats(int encoder, double* out, int n);
+int ivc_store_pace_reset_stats(void);
 
 /* ---------------------------------------------------------------- DCT -------------- */
 /* 2-D DCT-II (inverse=0) / DCT-III (inverse=1) of nblk contiguous 8x8 blocks, applied along
@@ -179,6 +187,16 @@ int ivc_histogram_i32_dev(const int32_t* sym, int64_t n, int32_t lo, int32_t nbi
 int ivc_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, int64_t* hist);
 int ivc_histogram_i64_dev(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
                           int64_t* hist, void* stream);
+/* stats_marg (ivclab/entropy/entropy.py:6-29) for any data and any bin edges:
+ * np.histogram(x, bins=edges) counts of float64 values x (the caller casts, as the reference
+ * does with image.astype(np.float64)) over nedges sorted float64 edges: x counts in bin i
+ * when edges[i] <= x < edges[i+1], x == edges[nedges-1] in the last bin, values outside and
+ * NaN dropped.  counts (nedges - 1 int64) are accumulated onto.  Edges that decrease are
+ * refused with NumPy's message (host entry point; the _dev form expects sorted edges).     */
+int ivc_histogram_f64_edges(const double* x, int64_t n, const double* edges, int32_t nedges,
+                            int64_t* counts);
+int ivc_histogram_f64_edges_dev(const double* x, int64_t n, const double* edges, int32_t nedges,
+                                int64_t* counts, void* stream);
 /* Workgroups per CU of the histogram launches (default 4, which fills the chip; 0 restores
  * the default).  A histogram on a side stream next to a VALU-bound kernel (the frame-sharded
  * bench step overlaps chunk k's histogram with chunk k+1's motion search) runs better with

@@ -39,6 +39,7 @@ _ALIASES = {
     "ivclab.utils": "ivclab_amd.utils",
     "ivclab.utils.shape": "ivclab_amd.utils.shape",
     "ivclab.utils.metrics": "ivclab_amd.utils.metrics",
+    "ivclab.utils.io": "ivclab_amd.utils.io",
     "ivclab.video": "ivclab_amd.video",
     "ivclab.video.motion": "ivclab_amd.video.motion",
     "ivclab.video.videocodec": "ivclab_amd.video.videocodec",

@@ -44,6 +44,8 @@ _SIGS = {
     "ivc_set_store_pace": ([_ct.c_double], _I),
     "ivc_store_pace": ([], _ct.c_double),
     "ivc_store_pace_late": ([], _ct.c_double),
+    "ivc_store_pace_stats": ([_I, _P, _I], _I),
+    "ivc_store_pace_reset_stats": ([], _I),
     "ivc_set_histogram_occupancy": ([_I], _I),
     "ivc_histogram_occupancy": ([], _I),
     "ivc_dct8x8": ([_P, _I, _L, _P, _I, _I, _I], _I),
@@ -67,6 +69,8 @@ _SIGS = {
     "ivc_histogram_i32": ([_P, _L, _ct.c_int32, _ct.c_int32, _P], _I),
     "ivc_histogram_i32_dev": ([_P, _L, _ct.c_int32, _ct.c_int32, _P, _P], _I),
     "ivc_histogram_i64": ([_P, _L, _L, _ct.c_int32, _P], _I),
+    "ivc_histogram_f64_edges": ([_P, _L, _P, _ct.c_int32, _P], _I),
+    "ivc_histogram_f64_edges_dev": ([_P, _L, _P, _ct.c_int32, _P, _P], _I),
     "ivc_huffman_lengths": ([_P, _ct.c_int32, _P], _I),
     "ivc_huffman_encode": ([_P, _L, _ct.c_int32, _P, _ct.c_int32, _P, _L, _P], _I),
     "ivc_huffman_decode": ([_P, _L, _L, _ct.c_int32, _P, _ct.c_int32, _P], _I),
@@ -162,6 +166,20 @@ def check(status: int, what: str = "ivc") -> None:
 
 def ptr(a: np.ndarray) -> int:
     return a.ctypes.data
+
+
+def pace_stats(encoder: int = 0):
+    """Store-pacing measurements of the current device since the last reset
+    (ivc_store_pace_stats), as a dict; None when no launch was measured."""
+    out = np.zeros(8, np.float64)
+    n = lib().ivc_store_pace_stats(encoder, out.ctypes.data, 8)
+    check(min(n, 0), "pace_stats")
+    if out[0] < 1:
+        return None
+    return {"launches_measured": int(out[0]), "launches_over_late_threshold": int(out[1]),
+            "late_fraction_mean": round(float(out[2]), 4), "late_fraction_max": round(float(out[3]), 4),
+            "rate_GBs": round(float(out[4]), 1), "late_fraction_last": round(float(out[5]), 4),
+            "achieved_GBs_mean": round(float(out[6]), 1)}
 
 
 def table_arg(table: np.ndarray) -> np.ndarray:

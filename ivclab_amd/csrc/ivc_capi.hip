@@ -205,6 +205,17 @@ double ivc_store_pace(void) { return store_pace_gbps(); }
 
 double ivc_store_pace_late(void) { return store_pace_late_fraction(); }
 
+int ivc_store_pace_stats(int encoder, double* out, int n) {
+  if (encoder < 0 || encoder > 1 || n < 0 || (n > 0 && !out))
+    return fail(IVC_E_ARG, "ivc_store_pace_stats: encoder must be 0 or 1, out must hold n values");
+  return store_pace_stats(encoder, out, n);
+}
+
+int ivc_store_pace_reset_stats(void) {
+  store_pace_reset_stats();
+  return IVC_OK;
+}
+
 int ivc_set_histogram_occupancy(int wg_per_cu) {
   if (wg_per_cu < 0 || wg_per_cu > 16)
     return fail(IVC_E_ARG, "ivc_set_histogram_occupancy: wg_per_cu must be in [0, 16]");
@@ -784,6 +795,31 @@ int ivc_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins, 
                                        st.ctx->stream), "histogram"));
   TRY(st.out(hist, d_hist, hb));
   return st.sync();
+}
+
+int ivc_histogram_f64_edges(const double* x, int64_t n, const double* edges, int32_t nedges,
+                            int64_t* counts) {
+  CHECK(n >= 0 && nedges >= 2, IVC_E_ARG, "histogram_f64_edges: need n >= 0 and >= 2 edges");
+  for (int32_t i = 0; i + 1 < nedges; ++i)
+    CHECK(!(edges[i] > edges[i + 1]), IVC_E_ARG, "`bins` must increase monotonically, when an array");
+  Staging st;
+  TRY(st.open());
+  const size_t cb = (size_t)(nedges - 1) * 8;
+  void* d_x = st.in(x, (size_t)n * 8);
+  void* d_e = st.in(edges, (size_t)nedges * 8);
+  int64_t* d_c = (int64_t*)st.in(counts, cb);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_edge_histogram((const double*)d_x, n, (const double*)d_e, nedges, d_c,
+                                        st.ctx->stream), "histogram_f64_edges"));
+  TRY(st.out(counts, d_c, cb));
+  return st.sync();
+}
+
+int ivc_histogram_f64_edges_dev(const double* x, int64_t n, const double* edges, int32_t nedges,
+                                int64_t* counts, void* stream) {
+  CHECK(n >= 0 && nedges >= 2, IVC_E_ARG, "histogram_f64_edges: need n >= 0 and >= 2 edges");
+  return dev_launch(launch_edge_histogram(x, n, edges, nedges, counts, (hipStream_t)stream),
+                    "histogram_f64_edges");
 }
 
 }  // extern "C"

@@ -610,4 +610,70 @@ hipError_t launch_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm, hipStre
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------- edge histogram ----
+// stats_marg's np.histogram(image.astype(float64).flatten(), bins=edges) (entropy.py:22-25)
+// for any sorted float64 edges: value x counts in bin i when edges[i] <= x < edges[i+1], the
+// last bin closed (x == edges[-1] counts in it), everything else (outside, NaN) dropped —
+// the comparisons np.histogram's searchsorted path makes, exactly.  Per value: a binary
+// search for the first edge > x.  Edges and per-workgroup counts in LDS when they fit
+// (EDGE_LDS_MAX edges), else the edges are read through the caches and the counts go to
+// global atomics.
+constexpr int EDGE_LDS_MAX = 4096;
+
+template <bool LDS>
+__global__ __launch_bounds__(256) void edge_histogram_kernel(const double* __restrict__ x,
+                                                             int64_t n,
+                                                             const double* __restrict__ edges_g,
+                                                             int nedges,
+                                                             unsigned long long* __restrict__ counts) {
+  __shared__ double e_s[LDS ? EDGE_LDS_MAX : 1];
+  __shared__ unsigned int c_s[LDS ? EDGE_LDS_MAX : 1];
+  const int nb = nedges - 1;
+  const double* edges = edges_g;
+  if (LDS) {
+    for (int i = threadIdx.x; i < nedges; i += 256) e_s[i] = edges_g[i];
+    for (int i = threadIdx.x; i < nb; i += 256) c_s[i] = 0;
+    __syncthreads();
+    edges = e_s;
+  }
+  const double lo = edges[0], hi = edges[nb];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const double v = __builtin_nontemporal_load(x + i);
+    if (!(v >= lo && v <= hi)) continue;                  // outside or NaN: dropped
+    int b;
+    if (v == hi) {
+      b = nb - 1;                                         // the closed last bin
+    } else {
+      int l = 0, r = nedges;                              // first edge > v lies in (0, nedges)
+      while (r - l > 1) {
+        const int m = (l + r) >> 1;
+        if (edges[m] <= v) l = m; else r = m;
+      }
+      b = l;
+    }
+    if (LDS) atomicAdd(&c_s[b], 1u);
+    else atomicAdd(&counts[b], 1ull);
+  }
+  if (LDS) {
+    __syncthreads();
+    for (int j = threadIdx.x; j < nb; j += 256)
+      if (c_s[j]) atomicAdd(&counts[j], (unsigned long long)c_s[j]);
+  }
+}
+
+hipError_t launch_edge_histogram(const double* x, int64_t n, const double* edges, int32_t nedges,
+                                 int64_t* counts, hipStream_t s) {
+  if (n <= 0 || nedges < 2) return hipSuccess;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  int64_t g = (n + 256 * 16 - 1) / (256 * 16);
+  if (g > (int64_t)cus * 4) g = (int64_t)cus * 4;
+  if (g < 1) g = 1;
+  auto* c = reinterpret_cast<unsigned long long*>(counts);
+  if (nedges <= EDGE_LDS_MAX) edge_histogram_kernel<true><<<(unsigned)g, 256, 0, s>>>(x, n, edges, nedges, c);
+  else edge_histogram_kernel<false><<<(unsigned)g, 256, 0, s>>>(x, n, edges, nedges, c);
+  return hipGetLastError();
+}
+
 }  // namespace ivc

@@ -42,6 +42,8 @@ hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, in
 double store_pace_gbps();
 double store_pace_late_fraction();
 void set_store_pace_gbps(double gbps);
+int store_pace_stats(int kind, double* out, int n);
+void store_pace_reset_stats();
 // workgroups per CU of the histogram launches (ivc_kernels.hip)
 int histogram_wg_per_cu();
 void set_histogram_wg_per_cu(int k);
@@ -74,6 +76,8 @@ hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected
                                  hipStream_t s);
 hipError_t launch_histogram_i64(const int64_t* sym, int64_t n, int64_t lo, int32_t nbins,
                                 int64_t* hist, hipStream_t s);
+hipError_t launch_edge_histogram(const double* x, int64_t n, const double* edges, int32_t nedges,
+                                 int64_t* counts, hipStream_t s);
 hipError_t launch_histogram(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins,
                             int64_t* hist, hipStream_t s);
 

@@ -1005,25 +1005,41 @@ static unsigned resident_grid(K kernel, int64_t work_groups_needed) {
 }
 
 // Store pacing of the coefficient-writing fused kernels (see pace_until).  The rate is the
-// total HBM rate (input + output bytes) the paced sweep is timed for.  It adapts per device
-// between launches: a launch whose late slots exceed PACE_LATE_HI of its slots lowers it by
-// 2% and marks it too fast; otherwise it creeps up by 0.5%, never past 99% of the lowest rate
-// seen too fast (a mark that itself rises 0.2% per good launch).  A launch's late count is read back without blocking (a pinned host copy
-// behind an event) when a later launch is set up.  IVC_PACE_GBPS / ivc_set_store_pace set the
-// starting rate (0 disables pacing).
+// total HBM rate (input + output bytes) the paced sweep is timed for, per device and encoder.
+// Every paced launch is measured (a ring of PACE_RING slots: the launch's late-slot counters
+// copied to pinned memory and its duration from two events), and completed measurements are
+// folded in launch order when a later launch is set up, or when the statistics are read:
+//  * late slots above PACE_LATE_HI of the launch's slots: the schedule outran the device.
+//    The rate drops to the lower of 98% of itself and 98.5% of what that launch actually
+//    moved (bytes / duration) — one measured launch brings a start rate that is far too fast
+//    back under the device's pace — and the launch's rate becomes the "too fast" mark;
+//  * otherwise the rate creeps up (+1.5% per launch while under 97% of the mark, +0.3%
+//    nearer it), never past 99% of the mark, which itself rises 0.2% per good launch so a
+//    transient cannot cap the rate for good.
+// IVC_PACE_GBPS / ivc_set_store_pace set the starting rate (0 disables pacing).
 static std::mutex g_pace_mu;
 static double g_pace_start = -1.0;
 // late-slot fractions are bimodal: < 1% below the device's rate, 20-50% once over it
 constexpr double PACE_LATE_HI = 0.05, PACE_MAX_GBPS = 7600.0;
+constexpr int PACE_RING = 32;
 
+struct PaceSlot {
+  uint64_t* host = nullptr;       // pinned copy of the late counters
+  hipEvent_t t0 = nullptr, t1 = nullptr;  // around the kernel (timing)
+  hipEvent_t done = nullptr;      // after the counters' copy
+  double slots = 0, bytes = 0, rate = 0;
+};
+struct PaceStats {
+  int64_t measured = 0, over = 0;
+  double sum_late = 0, max_late = 0, sum_gbps = 0;
+};
 struct PaceState {
   uint64_t* blk = nullptr;        // device pace block
-  uint64_t* host = nullptr;       // pinned copy of the late counters
-  hipEvent_t ev = nullptr;
-  bool pending = false;           // a measured launch's counters are on their way
-  bool arm = false;               // the launch being set up is the one to measure
-  double slots = 0;               // slots of the measured launch
+  PaceSlot ring[PACE_RING];
+  int head = 0, count = 0;        // oldest in-flight measurement, number in flight
+  int armed = -1;                 // slot of the launch being set up
   double rate = 0, too_fast = 1e30, last_late = -1;
+  PaceStats st;
 };
 // per device and per encoder (0: image source, 1: inter residual source)
 static PaceState g_pace[64][2];
@@ -1037,19 +1053,85 @@ static double pace_start_rate() {
   return g_pace_start;
 }
 
+// Folds every completed measurement, oldest first (caller holds g_pace_mu).
+static void pace_harvest(PaceState& P) {
+  while (P.count > 0) {
+    PaceSlot& S = P.ring[P.head];
+    if (hipEventQuery(S.done) != hipSuccess) break;
+    uint64_t late = 0;
+    for (int i = 0; i < PACE_SHARDS; ++i) late += S.host[i];
+    float ms = 0;
+    const bool timed = hipEventElapsedTime(&ms, S.t0, S.t1) == hipSuccess && ms > 0;
+    const double f = (double)late / S.slots;
+    const double gbps = timed ? S.bytes / (ms * 1e-3) / 1e9 : 0.0;
+    P.last_late = f;
+    P.st.measured += 1;
+    P.st.sum_late += f;
+    P.st.max_late = std::max(P.st.max_late, f);
+    P.st.sum_gbps += gbps;
+    if (f > PACE_LATE_HI) {
+      P.st.over += 1;
+      P.too_fast = std::min(P.too_fast, S.rate);
+      double r = P.rate * 0.98;
+      if (gbps > 0) r = std::min(r, 0.985 * gbps);
+      P.rate = std::max(r, 100.0);
+    } else {
+      P.too_fast *= 1.002;
+      const double cap = std::min(PACE_MAX_GBPS, 0.99 * P.too_fast);
+      const double step = P.rate < 0.97 * P.too_fast ? 1.015 : 1.003;
+      P.rate = std::max(std::min(P.rate * step, cap), P.rate);
+    }
+    P.head = (P.head + 1) % PACE_RING;
+    P.count -= 1;
+  }
+  (void)hipGetLastError();
+}
+
+static PaceState* pace_state_current(int kind) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  return &g_pace[dev][kind];
+}
+
 double store_pace_gbps() {
   std::lock_guard<std::mutex> g(g_pace_mu);
-  int dev = 0;
-  if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 64 && g_pace[dev][0].blk)
-    return g_pace[dev][0].rate;
+  PaceState* P = pace_state_current(0);
+  if (P && P->blk) {
+    pace_harvest(*P);
+    return P->rate;
+  }
   return pace_start_rate();
 }
 
 double store_pace_late_fraction() {
   std::lock_guard<std::mutex> g(g_pace_mu);
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
-  return g_pace[dev][0].last_late;
+  PaceState* P = pace_state_current(0);
+  if (!P) return -1;
+  if (P->blk) pace_harvest(*P);
+  return P->last_late;
+}
+
+int store_pace_stats(int kind, double* out, int n) {
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  PaceState* P = pace_state_current(kind);
+  if (!P) return 0;
+  if (P->blk) pace_harvest(*P);
+  const PaceStats& s = P->st;
+  const double m = s.measured > 0 ? (double)s.measured : 1.0;
+  const double v[8] = {(double)s.measured, (double)s.over, s.sum_late / m, s.max_late,
+                       P->blk ? P->rate : pace_start_rate(), P->last_late, s.sum_gbps / m,
+                       (double)P->count};
+  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
+  return n < 8 ? n : 8;
+}
+
+void store_pace_reset_stats() {
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  for (auto& d : g_pace)
+    for (auto& p : d) {
+      if (p.blk) pace_harvest(p);
+      p.st = PaceStats();
+    }
 }
 
 void set_store_pace_gbps(double gbps) {
@@ -1060,6 +1142,20 @@ void set_store_pace_gbps(double gbps) {
       p.rate = g_pace_start;
       p.too_fast = 1e30;
     }
+}
+
+static bool pace_alloc(PaceState& P) {
+  if (hipMalloc((void**)&P.blk, 8 * (1 + PACE_SHARDS)) != hipSuccess) {
+    P.blk = nullptr;
+    return false;
+  }
+  for (auto& S : P.ring) {
+    if (hipHostMalloc((void**)&S.host, 8 * PACE_SHARDS, hipHostMallocDefault) != hipSuccess ||
+        hipEventCreate(&S.t0) != hipSuccess || hipEventCreate(&S.t1) != hipSuccess ||
+        hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess)
+      return false;  // blk stays set: the ring is partially usable, never freed (process-long)
+  }
+  return true;
 }
 
 // Turns pacing on for a launch of `nwaves` persistent waves that store `slots` groups each
@@ -1075,58 +1171,50 @@ static void setup_pacing(FusedArgs& a, int kind, int64_t nwaves, int64_t slots,
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
   std::lock_guard<std::mutex> g(g_pace_mu);
   PaceState& P = g_pace[dev][kind];
+  P.armed = -1;
   if (!P.blk) {
     if (pace_start_rate() <= 0) return;
-    if (hipMalloc((void**)&P.blk, 8 * (1 + PACE_SHARDS)) != hipSuccess ||
-        hipHostMalloc((void**)&P.host, 8 * PACE_SHARDS, hipHostMallocDefault) != hipSuccess ||
-        hipEventCreateWithFlags(&P.ev, hipEventDisableTiming) != hipSuccess) {
+    if (!pace_alloc(P)) {
       (void)hipGetLastError();
-      P.blk = nullptr;
-      return;
+      if (!P.blk) return;
     }
     P.rate = pace_start_rate();
   }
-  if (P.pending && hipEventQuery(P.ev) == hipSuccess) {
-    uint64_t late = 0;
-    for (int i = 0; i < PACE_SHARDS; ++i) late += P.host[i];
-    P.last_late = (double)late / P.slots;
-    if (P.last_late > PACE_LATE_HI) {
-      P.too_fast = std::min(P.too_fast, P.rate);
-      P.rate *= 0.98;
-    } else {
-      P.too_fast *= 1.002;       // forget slowly: a transient must not cap the rate for good
-      const double cap = std::min(PACE_MAX_GBPS, 0.99 * P.too_fast);
-      P.rate = std::max(std::min(P.rate * 1.005, cap), P.rate);
-    }
-    P.pending = false;
-  }
-  (void)hipGetLastError();
+  pace_harvest(P);
   if (P.rate <= 0) return;
   // ticks (10 ns) per slot: the whole grid's slot bytes at the target rate
   const double d256 = (double)nwaves * group_bytes / (P.rate * 1e9) * 1e8 * 256.0;
   if (!(d256 >= 1.0) || d256 > 4.0e9) return;
+  if (P.count < PACE_RING) {
+    const int k = (P.head + P.count) % PACE_RING;
+    PaceSlot& S = P.ring[k];
+    if (S.host && S.done && hipEventRecord(S.t0, s) == hipSuccess) {
+      S.slots = (double)nwaves * (double)slots;
+      S.bytes = (double)nwaves * (double)slots * group_bytes;
+      S.rate = P.rate;
+      P.armed = k;
+    }
+    (void)hipGetLastError();
+  }
   pace_stamp_kernel<<<1, 1, 0, s>>>(P.blk, 300u);
   a.pace_t0 = P.blk;
   a.pace_d = (uint32_t)d256;
-  if (!P.pending) {
-    P.slots = (double)nwaves * (double)slots;
-    P.pending = P.arm = true;
-  }
 }
 
-// After a paced launch: queue the copy-back of its late counters if it is the measured one.
+// After a paced launch: close its measurement (end event, counters' copy, done event).
 static void finish_pacing(int kind, hipStream_t s) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
   std::lock_guard<std::mutex> g(g_pace_mu);
   PaceState& P = g_pace[dev][kind];
-  if (!P.arm) return;
-  P.arm = false;
-  if (hipMemcpyAsync(P.host, P.blk + 1, 8 * PACE_SHARDS, hipMemcpyDeviceToHost, s) != hipSuccess ||
-      hipEventRecord(P.ev, s) != hipSuccess) {
-    (void)hipGetLastError();
-    P.pending = false;
-  }
+  if (P.armed < 0) return;
+  PaceSlot& S = P.ring[P.armed];
+  P.armed = -1;
+  if (hipEventRecord(S.t1, s) == hipSuccess &&
+      hipMemcpyAsync(S.host, P.blk + 1, 8 * PACE_SHARDS, hipMemcpyDeviceToHost, s) == hipSuccess &&
+      hipEventRecord(S.done, s) == hipSuccess)
+    P.count += 1;
+  (void)hipGetLastError();
 }
 
 // NG: groups of 8 blocks per wave load (wide, whole-cache-line row loads for u8 luma)

@@ -37,33 +37,50 @@ def entropy_bits(pmf):
 
 def stats_marg(image, pixel_range):
     """entropy.py:6-29 — np.histogram(image.astype(float64).flatten(), bins=pixel_range)
-    / image.size — for integer images over unit-spaced integer edges (the symbol and pixel
-    statistics of the codec), counted by the GPU histogram kernel.  np.histogram drops values
+    / image.size, counted on the GPU.
+
+    Integer images over unit-spaced integer edges (the symbol and pixel statistics of the
+    codec) take the integer histogram kernel on the raw values: np.histogram drops values
     outside [edges[0], edges[-1]] and closes the last bin; the kernel clamps, so two guard
     bins on each side absorb the out-of-range values and the top edge value is folded into
-    the last bin."""
+    the last bin.  Everything else — float images, any edges, an int bin count or a binning
+    rule — takes the edge kernel on the float64-cast values over the edges np.histogram
+    itself would use (np.histogram_bin_edges: same validation, same errors), with
+    np.histogram's comparisons: edges[i] <= x < edges[i+1], last bin closed, NaN and
+    out-of-range values dropped."""
     from .. import _native as N
     a = np.asarray(image)
     edges = np.asarray(pixel_range)
-    if not (np.issubdtype(a.dtype, np.integer) or a.dtype == np.bool_):
-        raise NotImplementedError("stats_marg: integer images only")
-    if edges.ndim != 1 or edges.size < 2 or not np.issubdtype(edges.dtype, np.integer) or \
-            np.any(np.diff(edges) != 1):
-        raise NotImplementedError("stats_marg: unit-spaced integer bin edges only")
-    lo, nb = int(edges[0]), edges.size - 1
-    x = np.ascontiguousarray(a.ravel())
-    hist = np.zeros(nb + 3, np.int64)                  # [< lo | lo .. lo+nb-1 | lo+nb | > lo+nb]
-    if x.dtype.itemsize <= 4 and x.dtype != np.uint32:
-        x32 = x.astype(np.int32, copy=False)
-        N.check(N.lib().ivc_histogram_i32(N.ptr(x32), x32.size, lo - 1, nb + 3, N.ptr(hist)),
-                "stats_marg")
-    else:
-        x64 = x.astype(np.int64, copy=False)
-        N.check(N.lib().ivc_histogram_i64(N.ptr(x64), x64.size, lo - 1, nb + 3, N.ptr(hist)),
-                "stats_marg")
-    counts = hist[1:nb + 1].copy()
-    counts[-1] += hist[nb + 1]
-    return counts / x.size
+    unit_int = (edges.ndim == 1 and edges.size >= 2 and np.issubdtype(edges.dtype, np.integer)
+                and bool(np.all(np.diff(edges) == 1)))
+    # integers of up to 32 bits are exact in float64, so counting the raw values is the same
+    # as counting the reference's float64 casts; wider ones take the float path (the cast
+    # rounds beyond 2^53, as the reference's does)
+    small_int = (np.issubdtype(a.dtype, np.integer) and a.dtype.itemsize <= 4) or a.dtype == np.bool_
+    if unit_int and small_int:
+        lo, nb = int(edges[0]), edges.size - 1
+        x = np.ascontiguousarray(a.ravel())
+        hist = np.zeros(nb + 3, np.int64)              # [< lo | lo .. lo+nb-1 | lo+nb | > lo+nb]
+        if x.dtype != np.uint32:
+            x32 = x.astype(np.int32, copy=False)
+            N.check(N.lib().ivc_histogram_i32(N.ptr(x32), x32.size, lo - 1, nb + 3, N.ptr(hist)),
+                    "stats_marg")
+        else:
+            x64 = x.astype(np.int64, copy=False)
+            N.check(N.lib().ivc_histogram_i64(N.ptr(x64), x64.size, lo - 1, nb + 3, N.ptr(hist)),
+                    "stats_marg")
+        counts = hist[1:nb + 1].copy()
+        counts[-1] += hist[nb + 1]
+        return counts / x.size
+    flat = np.ascontiguousarray(a.astype(np.float64).flatten())
+    bin_edges = np.ascontiguousarray(np.histogram_bin_edges(flat, bins=pixel_range), np.float64)
+    if bin_edges.size - 1 > np.iinfo(np.int32).max:
+        raise ValueError("stats_marg: too many bins")
+    counts = np.zeros(bin_edges.size - 1, np.int64)
+    if flat.size and counts.size:
+        N.check(N.lib().ivc_histogram_f64_edges(N.ptr(flat), flat.size, N.ptr(bin_edges),
+                                                bin_edges.size, N.ptr(counts)), "stats_marg")
+    return counts / flat.size
 
 
 def calc_entropy(pmf, eps=1e-8):

@@ -340,9 +340,8 @@ def zerorun_decode(encoded, original_shape, eob=4000, block_size=64):
 def stats_marg(image, pixel_range):
     """stats_marg (ivclab/entropy/entropy.py:6-29): np.histogram of the float64-cast,
     flattened data over the bin edges pixel_range, divided by the number of samples.
-    (The module is not importable here — it imports ivclab.utils, whose package __init__
-    needs the absent constriction wheel — so this restatement is pinned by the same NumPy
-    calls, not by fixtures.)"""
+    Pinned by tests/golden/stats.npz (the reference's own stats_marg, imported with the
+    `ivclab` / `ivclab.entropy` package __init__ files bypassed: make_golden.py make_stats)."""
     flat = np.asarray(image).astype(np.float64).flatten()
     counts, _ = np.histogram(flat, bins=pixel_range)
     return counts / flat.size
@@ -353,6 +352,12 @@ def smooth_pmf(pmf, epsilon=1e-9):
     pmf = pmf + epsilon
     pmf /= pmf.sum()
     return pmf
+
+
+def calc_entropy(pmf):
+    """entropy.py:36-51."""
+    nonzero_pmf = pmf[pmf > 0]
+    return -np.sum(nonzero_pmf * np.log2(nonzero_pmf))
 
 
 # ---------------------------------------------------------------- colour ----------------

@@ -17,6 +17,15 @@ Reference modules used (paths relative to /root/reference):
   ivclab/entropy/zerorun.py       ZeroRunCoder (zerorun.npz; its own RNG stream, so the
                                   other fixtures are unchanged by its addition)
   ivclab/signal/color.py          rgb2gray, rgb2ycbcr, ycbcr2rgb (color.npz; own RNG stream)
+  ivclab/entropy/entropy.py       stats_marg, smooth_pmf, calc_entropy (stats.npz; imported as
+                                  ivclab.entropy.entropy with the `ivclab` and `ivclab.entropy`
+                                  package __init__ files bypassed — they import huffman.py,
+                                  which needs the absent `constriction`)
+  ivclab/utils/metrics.py         calc_mse, calc_psnr (ch3.npz: the quantities tests/ch3.py:18-47
+                                  asserts, computed by the reference on a synthetic stand-in for
+                                  the absent data/satpic1.bmp, written as satpic_standin.bmp)
+
+    python tests/golden/make_golden.py [ch3 ...]   # only the named fixture groups
 """
 import contextlib
 import importlib.util
@@ -197,6 +206,8 @@ def main():
     np.savez_compressed(os.path.join(OUT, "intra.npz"), **p)
     make_zerorun(p)
     make_color()
+    make_ch3()
+    make_stats()
     for f in sorted(os.listdir(OUT)):
         if f.endswith(".npz"):
             print(f, os.path.getsize(os.path.join(OUT, f)))
@@ -294,5 +305,99 @@ def make_color():
     np.savez_compressed(os.path.join(OUT, "color.npz"), **c)
 
 
+def satpic_standin(rng, H=256, W=256):
+    """A synthetic 'satellite picture' (RGB uint8): smooth terrain-like fields per channel at
+    two scales, field-boundary edges, and sensor noise."""
+    def smooth(n):
+        lo = rng.normal(0, 1, (H // n + 2, W // n + 2))
+        return np.kron(lo, np.ones((n, n)))[:H, :W]
+    y = 110 + 45 * smooth(32) + 20 * smooth(8)
+    fields = (smooth(16) > 0.3) * 35
+    img = np.stack([y + fields + 10 * smooth(4) * c for c in (0.8, 1.0, 0.6)], axis=-1)
+    img += rng.normal(0, 6, img.shape)
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8)
+
+
+def make_ch3():
+    """tests/ch3.py:18-47 on a committed synthetic stand-in for data/satpic1.bmp: the BMP
+    (read back through PIL exactly as ivclab.utils.imread does, io.py:5-8) and the quantities
+    the reference's own modules compute for each assertion."""
+    from PIL import Image
+    dct_m = _load("ivclab/signal/dct.py", "ref_dct")
+    pq_m = _load("ivclab/quantization/patchquant.py", "ref_patchquant")
+    sh_m = _load("ivclab/utils/shape.py", "ref_shape")
+    me_m = _load("ivclab/utils/metrics.py", "ref_metrics")
+    img = satpic_standin(np.random.default_rng(31415))
+    path = os.path.join(OUT, "satpic_standin.bmp")
+    Image.fromarray(img).save(path)
+    with Image.open(path) as data:
+        orig = np.asarray(data)
+    assert np.array_equal(orig, img)
+    P = sh_m.Patcher(window_size=(8, 8))
+    D = dct_m.DiscreteCosineTransform(norm="ortho")
+    Q = pq_m.PatchQuant(quantization_scale=1.0)
+    patched = P.patch(orig)
+    transformed = D.transform(patched)
+    quantized = Q.quantize(patched)
+    rec = P.unpatch(Q.dequantize(quantized))
+    c = {"mean_energy": np.float64(np.mean(transformed ** 2)),
+         "inverse_allclose": np.bool_(np.allclose(D.inverse_transform(transformed), patched)),
+         "mean_q2": np.float64(np.mean(quantized ** 2)),
+         "mse": np.float64(me_m.calc_mse(orig, rec)),
+         "psnr": np.float64(me_m.calc_psnr(orig, rec))}
+    np.savez_compressed(os.path.join(OUT, "ch3.npz"), **c)
+    print({k: float(v) for k, v in c.items()})
+
+
+def _load_package_module(dotted):
+    """Import ivclab.<...> with the reference's package __init__ files of `ivclab` and
+    `ivclab.entropy` bypassed (they pull in huffman.py -> the absent `constriction` wheel);
+    every other module, __init__ included, runs as in the reference."""
+    import types
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    for pkg in ("ivclab", "ivclab.entropy"):
+        if pkg not in sys.modules:
+            m = types.ModuleType(pkg)
+            m.__path__ = [os.path.join(REF, *pkg.split("."))]
+            sys.modules[pkg] = m
+    return importlib.import_module(dotted)
+
+
+def make_stats():
+    """stats_marg / smooth_pmf / calc_entropy fixtures (ivclab/entropy/entropy.py:6-51):
+    integer images over unit edges, non-integer float images over float / non-uniform edges,
+    an int bin count, NaN and +-inf samples, values on the closing edge."""
+    en = _load_package_module("ivclab.entropy.entropy")
+    rng = np.random.default_rng(77)
+    s = {}
+    cases = {
+        "u8_full": (rng.integers(0, 256, (40, 50, 3)).astype(np.uint8), np.arange(256)),
+        "i16_window": (rng.integers(-300, 300, (60, 70)).astype(np.int16), np.arange(-20, 41)),
+        "i64_unit": (rng.integers(-(1 << 40), 1 << 40, 500).astype(np.int64), np.arange(-5, 6)),
+        "f64_linspace": (rng.normal(128, 50, (64, 64)), np.linspace(0, 255, 52)),
+        "f32_nonuniform": (rng.normal(0, 3, (30, 40)).astype(np.float32),
+                           np.array([-9.0, -2.5, -1.0, -0.25, 0.0, 0.1, 1.0, 4.0, 9.5])),
+        "f64_intbins": (rng.normal(10, 2, 777), 17),
+        "f64_edges_special": (np.array([np.nan, 1.0, 2.0, 5.0, -np.inf, np.inf, 0.0, 4.999]),
+                              np.array([0.0, 1.0, 2.0, 5.0])),
+        "f64_inf_edges": (np.array([np.nan, 1.0, -np.inf, np.inf, 0.0]),
+                          np.array([-np.inf, 0.0, np.inf])),
+        "u8_float_edges": (rng.integers(0, 256, (32, 32)).astype(np.uint8), np.arange(0, 257, 4.0)),
+        "u8_step_edges": (rng.integers(0, 256, (32, 32)).astype(np.uint8), np.arange(0, 256, 3)),
+    }
+    for k, (x, bins) in cases.items():
+        s[f"{k}_x"] = x
+        s[f"{k}_bins"] = np.asarray(bins)
+        pmf = en.stats_marg(x, bins)
+        s[f"{k}_pmf"] = pmf
+        s[f"{k}_smooth"] = en.smooth_pmf(pmf)
+        s[f"{k}_entropy"] = np.float64(en.calc_entropy(pmf))
+    np.savez_compressed(os.path.join(OUT, "stats.npz"), **s)
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    parts = sys.argv[1:]
+    if not parts:
+        sys.exit(main())
+    for part in parts:
+        {"ch3": make_ch3, "stats": make_stats}[part]()

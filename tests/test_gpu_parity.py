@@ -947,3 +947,37 @@ def test_stats_marg_gpu_vs_oracle():
         x = rng.integers(-300 if dt != np.uint8 else 0, 256, (50, 60)).astype(dt)
         for edges in (np.arange(256), np.arange(-20, 41), np.arange(10, 12)):
             assert_bits(stats_marg(x, edges), O.stats_marg(x, edges), f"{dt} {edges[0]}")
+
+
+STATS = ["u8_full", "i16_window", "i64_unit", "f64_linspace", "f32_nonuniform", "f64_intbins",
+         "f64_edges_special", "f64_inf_edges", "u8_float_edges", "u8_step_edges"]
+
+
+@pytest.mark.parametrize("case", STATS)
+def test_stats_marg_golden_gpu(golden, case):
+    """The GPU stats_marg (integer kernel for small-integer data over unit edges, the edge
+    kernel for everything else) against the reference's own pmf, bit for bit."""
+    from ivclab_amd.entropy import calc_entropy, smooth_pmf, stats_marg
+    s = golden("stats")
+    x, bins = s[f"{case}_x"], s[f"{case}_bins"]
+    bins = int(bins) if bins.ndim == 0 else bins
+    pmf = stats_marg(x, bins)
+    assert_bits(pmf, s[f"{case}_pmf"], case)
+    assert_bits(smooth_pmf(pmf), s[f"{case}_smooth"], case)
+    assert_bits(np.float64(calc_entropy(pmf)), s[f"{case}_entropy"], case)
+
+
+def test_stats_marg_edge_kernel_large_and_errors():
+    """The edge kernel past its LDS capacity (5000 edges: global path), on 2M non-integer
+    samples, and np.histogram's errors (decreasing edges, a non-finite autodetected range)."""
+    from ivclab_amd.entropy import stats_marg
+    rng = np.random.default_rng(5)
+    x = rng.normal(0, 40, (1000, 2000))
+    x[::97, ::13] = np.nan
+    for edges in (np.linspace(-100, 100, 5000), np.sort(rng.normal(0, 50, 300)), np.array([0.0, 0.0, 1.0])):
+        assert_bits(stats_marg(x, edges), O.stats_marg(x, edges), f"{edges.size} edges")
+    assert_bits(stats_marg(x[1:8].astype(np.float32), 33), O.stats_marg(x[1:8].astype(np.float32), 33))
+    with pytest.raises(ValueError):
+        stats_marg(x, np.array([3.0, 2.0, 1.0]))
+    with pytest.raises(ValueError):
+        stats_marg(np.array([1.0, np.nan]), 4)

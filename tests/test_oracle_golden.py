@@ -169,3 +169,39 @@ def test_rgb2ycbcr_is_korder_fma(golden):
     for k in ("rgb_u8", "rgb_f64"):
         x = c[k][:6, :8]
         assert bits_equal(O.rgb2ycbcr_fma(x), c[f"{k}_ycc"][:6, :8]), k
+
+
+STATS = ["u8_full", "i16_window", "i64_unit", "f64_linspace", "f32_nonuniform", "f64_intbins",
+         "f64_edges_special", "f64_inf_edges", "u8_float_edges", "u8_step_edges"]
+
+
+@pytest.mark.parametrize("case", STATS)
+def test_stats_golden(golden, case):
+    """stats_marg / smooth_pmf / calc_entropy (entropy.py:6-51) against the reference's own
+    outputs: integer and float data, unit / float / non-uniform edges, an int bin count,
+    NaN and infinities, values on the closing edge."""
+    s = golden("stats")
+    x, bins = s[f"{case}_x"], s[f"{case}_bins"]
+    bins = int(bins) if bins.ndim == 0 else bins
+    pmf = O.stats_marg(x, bins)
+    assert bits_equal(pmf, s[f"{case}_pmf"])
+    assert bits_equal(O.smooth_pmf(pmf), s[f"{case}_smooth"])
+    assert bits_equal(np.float64(O.calc_entropy(pmf)), s[f"{case}_entropy"])
+
+
+def test_c_inter_encode_matches_oracle_chain():
+    """oracle.c_inter_encode (C ME + block copy + NumPy DCT/quant, row-restricted) equals
+    ivc_oracle.inter_encode, whole frame and on block-row stripes."""
+    from oracle import c_inter_encode
+    rng = np.random.default_rng(11)
+    a = rng.integers(0, 256, (48, 64), dtype=np.uint8)
+    b = np.roll(a, (2, -3), (0, 1))
+    b[5:20, 7:30] = rng.integers(0, 256, (15, 23))
+    for zz in (False, True):
+        mv, q = O.inter_encode(a, b, 4, 1.0, zz)
+        mv2, q2 = c_inter_encode(a, b, 4, 1.0, zz)
+        assert bits_equal(mv2, mv.astype(np.int64)) and bits_equal(q2, q)
+        for rows in ((0, 2), (2, 5), (5, 6)):
+            mv3, q3 = c_inter_encode(a, b, 4, 1.0, zz, rows=rows)
+            assert bits_equal(mv3, mv[rows[0]:rows[1]].astype(np.int64))
+            assert bits_equal(q3, q[rows[0]:rows[1]])
