@@ -537,7 +537,7 @@ def leg_inter_f64(args, dist, rank, world, dev, seq_u8, result, verify):
         "config": {"workload": f"{Fi} frames 1920x1080 non-integer float64 luma per GPU, sr={sr}, "
                                "MotionCompensator.compute_motion_vector semantics (pairwise "
                                "np.sum order, first strict minimum)"},
-        "roofline": {"bound": "valu (fp64)", "kernel": "me_f64 search", "kernel_ms": round(ms, 4),
+        "roofline": {"bound": "valu (fp64)", "kernel": "me_flt_kernel<double,16>", "kernel_ms": round(ms, 4),
                      "achieved": round(ops / (ms * 1e-3) / 1e12, 2), "peak": F64_PEAK_T,
                      "unit": "T fp64 op/s", "frac": round(ops / (ms * 1e-3) / 1e12 / F64_PEAK_T, 4),
                      "algorithmic_ops_per_launch": ops,

@@ -162,6 +162,191 @@ __global__ __launch_bounds__(256) void me_generic_kernel(const T* __restrict__ r
   }
 }
 
+// ---------------------------------------------------------------- float search -------
+// NumPy semantics for float32 / float64 frames (the ME VideoCodec runs on its non-integer
+// float64 luma, videocodec.py:38,52): every candidate's SSD in the reference's rounding order
+// (np.sum's pairwise order over the 64 contiguous squares: column sums down the rows, then
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7))), no fused multiply-add.
+//
+// A 512-thread workgroup takes a round of NB horizontally adjacent blocks of one block row:
+// the round's reference window (8 + 2sr rows x 8 NB + 2sr columns, zero outside the frame)
+// and its blocks (column-major) are staged in LDS; thread (b, e) owns block b's candidate
+// column dx = e - sr and walks its dy in runs of FLT_DY: per block column v it loads the
+// FLT_DY + 7 window values of column e + v once (each serves up to 8 candidates) and the
+// block's column v, and folds each candidate's column sum into its pairwise tree (three
+// partial sums live per candidate).  Lanes of neighbouring blocks read the same window
+// words (broadcast), and consecutive lanes consecutive words (conflict-free).  The block's
+// (SSD, raster index) minimum over its 2sr+1 threads: an LDS atomic minimum of the SSD bits
+// (non-negative doubles order like their bits), a barrier, then the minimum index among the
+// threads holding that SSD — the reference's first strict minimum.
+constexpr int FLT_WG = 512, FLT_DY = 11;
+
+template <typename T> struct FltBits;
+template <> struct FltBits<double> {
+  typedef unsigned long long U;
+  __device__ static U bits(double v) { return (U)__double_as_longlong(v); }
+};
+template <> struct FltBits<float> {
+  typedef unsigned int U;
+  __device__ static U bits(float v) { return (U)__float_as_uint(v); }
+};
+
+
+// An empty asm that takes the FLT_DY partial sums in and out (so they are computed before
+// it) and clobbers memory (so no LDS load moves above it).
+template <typename T>
+__device__ __forceinline__ void flt_pin(T (&a)[FLT_DY]) {
+  static_assert(FLT_DY == 11, "flt_pin lists FLT_DY operands");
+  __asm__ volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                   "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]) :: "memory");
+}
+
+// Round geometry: NBR blocks per round (2sr+1 threads each), capped so that the window, the
+// blocks and the minimum arrays fit FLT_LDS bytes (the default per-workgroup LDS limit).
+constexpr int FLT_LDS = 64 * 1024;
+template <typename T, int SR> struct FltGeom {
+  // WR window rows plus the rows a partial last dy run reads past them (zeros, never used)
+  static constexpr int N = 2 * SR + 1, WR = 8 + 2 * SR;
+  static constexpr int RUNS = (N + FLT_DY - 1) / FLT_DY, WRP = RUNS * FLT_DY + 7;
+  static constexpr int PER_NB = (WRP * 8 + 64) * (int)sizeof(T) + (int)sizeof(T) + 4;
+  static constexpr int NB_LDS = (FLT_LDS - WRP * 2 * SR * (int)sizeof(T)) / PER_NB;
+  static constexpr int NBR = FLT_WG / N < NB_LDS ? FLT_WG / N : NB_LDS;
+  static constexpr int WC = NBR * 8 + 2 * SR;
+  static constexpr size_t LDS = ((size_t)WRP * WC + (size_t)NBR * 64) * sizeof(T) +
+                                (size_t)NBR * (sizeof(T) + 4);
+  static_assert(NBR >= 1 && LDS <= (size_t)FLT_LDS, "round does not fit the LDS budget");
+};
+
+template <typename T, int SR>
+__global__ __launch_bounds__(FLT_WG, sizeof(T) == 8 ? 2 : 4) void me_flt_kernel(const T* __restrict__ ref,
+                                                           const T* __restrict__ cur,
+                                                           int64_t nframes, int H, int W,
+                                                           int64_t* __restrict__ mv) {
+  typedef typename FltBits<T>::U U;
+  typedef FltGeom<T, SR> G;
+  extern __shared__ __attribute__((aligned(16))) unsigned char flt_smem[];
+  constexpr int sr = SR, n = G::N, nbr = G::NBR, WR = G::WR, WC = G::WC, WRP = G::WRP;
+  const int h = H / 8, w = W / 8;
+  T* win = reinterpret_cast<T*>(flt_smem);                // [WRP][WC]
+  T* cb = win + WRP * WC;                                 // [nbr][v][u]
+  U* kmin = reinterpret_cast<U*>(cb + nbr * 64);          // [nbr]
+  unsigned* imin = reinterpret_cast<unsigned*>(kmin + nbr);
+  const int segs = (w + nbr - 1) / nbr;
+  const int64_t rounds = nframes * h * segs;
+  const int tid = threadIdx.x;
+  const int sb = tid / n, se = tid - sb * n;              // block of the round, candidate column
+  for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
+    const int64_t f = r / ((int64_t)h * segs);
+    const int rem = (int)(r - f * h * segs), by = rem / segs, bx0 = (rem - by * segs) * nbr;
+    const int nb = w - bx0 < nbr ? w - bx0 : nbr;
+    const T* rf = ref + f * (int64_t)H * W;
+    const T* cf = cur + f * (int64_t)H * W;
+    const int y0 = 8 * by - sr, x0 = 8 * bx0 - sr, wc = nb * 8 + 2 * sr;
+    for (int i = tid; i < WRP * wc; i += FLT_WG) {
+      const int yy = i / wc, xx = i - yy * wc, gy = y0 + yy, gx = x0 + xx;
+      win[yy * WC + xx] = (yy < WR && gy >= 0 && gy < H && gx >= 0 && gx < W)
+                              ? rf[(int64_t)gy * W + gx] : T(0);
+    }
+    for (int i = tid; i < nb * 64; i += FLT_WG) {
+      const int b = i >> 6, u = (i >> 3) & 7, v = i & 7;
+      cb[b * 64 + v * 8 + u] = cf[(int64_t)(8 * by + u) * W + 8 * (bx0 + b) + v];
+    }
+    for (int i = tid; i < nb; i += FLT_WG) {
+      kmin[i] = ~(U)0;
+      imin[i] = ~0u;
+    }
+    __syncthreads();
+    T best = T(0);
+    int bidx = -1;
+    const int rx = 8 * (bx0 + sb) + se - sr;
+    if (sb < nb && rx >= 0 && rx + 8 <= W) {
+      const T* cblk = cb + sb * 64;
+#pragma unroll 1
+      for (int dy0 = 0; dy0 < n; dy0 += FLT_DY) {
+        T ta[FLT_DY], tb[FLT_DY], tc[FLT_DY];
+#pragma unroll
+        for (int v = 0; v < 8; ++v) {
+          T cv[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) cv[u] = cblk[v * 8 + u];
+          const T* col = win + dy0 * WC + sb * 8 + se + v;
+          T rv[FLT_DY + 7];
+#pragma unroll
+          for (int k = 0; k < FLT_DY + 7; ++k) rv[k] = col[k * WC];
+#pragma unroll
+          for (int k = 0; k < FLT_DY; ++k) {
+            T d = cv[0] - rv[k];
+            T sk = d * d;
+#pragma unroll
+            for (int u = 1; u < 8; ++u) {
+              d = cv[u] - rv[k + u];
+              sk = sk + d * d;
+            }
+            // ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7))
+            if (v == 0) ta[k] = sk;
+            if (v == 1) ta[k] = ta[k] + sk;
+            if (v == 2 || v == 4) tb[k] = sk;
+            if (v == 3) ta[k] = ta[k] + (tb[k] + sk);
+            if (v == 5) tb[k] = tb[k] + sk;
+            if (v == 6) tc[k] = sk;
+            if (v == 7) tb[k] = tb[k] + (tc[k] + sk);
+          }
+          // keep the schedule column by column: the partial sums are finished here, before
+          // the next column's window loads (otherwise the compiler hoists every column's
+          // loads to the top and spills)
+          flt_pin<T>(ta);                      // live from column 0
+          if (v >= 2) flt_pin<T>(tb);          // from column 2
+          if (v == 6) flt_pin<T>(tc);          // columns 6-7 only
+        }
+#pragma unroll
+        for (int k = 0; k < FLT_DY; ++k) {
+          const int d = dy0 + k, ry = 8 * by + d - sr;
+          const T tot = ta[k] + tb[k];
+          // eligible: in frame and below the reference's initial float('inf'); first strict
+          // minimum in raster order (dy ascending within the thread)
+          if (d < n && ry >= 0 && ry + 8 <= H && tot < (T)INFINITY && (bidx < 0 || tot < best)) {
+            best = tot;
+            bidx = d * n + se;
+          }
+        }
+      }
+    }
+    if (bidx >= 0) atomicMin(&kmin[sb], FltBits<T>::bits(best));
+    __syncthreads();
+    if (bidx >= 0 && FltBits<T>::bits(best) == kmin[sb]) atomicMin(&imin[sb], (unsigned)bidx);
+    __syncthreads();
+    if (tid < nb)
+      mv[(f * h + by) * w + bx0 + tid] = imin[tid] == ~0u ? (int64_t)sr * n + sr : (int64_t)imin[tid];
+    __syncthreads();
+  }
+}
+
+template <typename T, int SR>
+static void launch_me_flt_sr(const T* ref, const T* cur, int64_t nframes, int64_t H, int64_t W,
+                             int64_t* mv, hipStream_t s) {
+  typedef FltGeom<T, SR> G;
+  const int w = (int)(W / 8), h = (int)(H / 8);
+  const int64_t rounds = nframes * h * ((w + G::NBR - 1) / G::NBR);
+  const size_t lds = G::LDS;
+  // f64: 144 VGPRs, one 512-thread workgroup per CU; f32: two (88 VGPRs, LDS permitting)
+  const unsigned grid = me_grid(rounds, 1, sizeof(T) == 4 && lds * 2 <= 160 * 1024 ? 2 : 1);
+  me_flt_kernel<T, SR><<<grid, FLT_WG, lds, s>>>(ref, cur, nframes, (int)H, (int)W, mv);
+}
+
+// The float search for the search ranges it is compiled for (window geometry is static, so
+// every LDS offset is an immediate); false sends the caller to the generic kernel.
+template <typename T>
+static bool launch_me_flt(const T* ref, const T* cur, int64_t nframes, int64_t H, int64_t W,
+                          int sr, int64_t* mv, hipStream_t s) {
+  if (H < 8 || W < 8) return false;
+  switch (sr) {
+    case 4: launch_me_flt_sr<T, 4>(ref, cur, nframes, H, W, mv, s); return true;
+    case 8: launch_me_flt_sr<T, 8>(ref, cur, nframes, H, W, mv, s); return true;
+    case 16: launch_me_flt_sr<T, 16>(ref, cur, nframes, H, W, mv, s); return true;
+    default: return false;
+  }
+}
+
 // ---------------------------------------------------------------- fast exact u8 search
 // Integer-valued u8 frames (IVC_ME_EXACT_U8 — the reference run on frame.astype(float64),
 // videocodec.py:38), search range SR in {4, 8, 16}.
@@ -560,8 +745,14 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
     case IVC_I32: ME_LAUNCH(int32_t, 0); break;
     case IVC_U64: ME_LAUNCH(uint64_t, 0); break;
     case IVC_I64: ME_LAUNCH(int64_t, 0); break;
-    case IVC_F32: ME_LAUNCH(float, 0); break;
-    case IVC_F64: ME_LAUNCH(double, 0); break;
+    case IVC_F32:
+      if (!launch_me_flt<float>((const float*)ref, (const float*)cur, nframes, H, W, sr, mv, s))
+        ME_LAUNCH(float, 0);
+      break;
+    case IVC_F64:
+      if (!launch_me_flt<double>((const double*)ref, (const double*)cur, nframes, H, W, sr, mv, s))
+        ME_LAUNCH(double, 0);
+      break;
     default: return hipErrorInvalidValue;
   }
 #undef ME_LAUNCH

@@ -981,3 +981,46 @@ def test_stats_marg_edge_kernel_large_and_errors():
         stats_marg(x, np.array([3.0, 2.0, 1.0]))
     with pytest.raises(ValueError):
         stats_marg(np.array([1.0, np.nan]), 4)
+
+
+@pytest.mark.parametrize("sr", [4, 8, 16])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_me_float_search_kernel(sr, dtype):
+    """The LDS-window float search (me_flt_kernel, sr in {4, 8, 16}) against the C oracle's
+    NumPy-order SSD: non-integer frames with a shift, an 8-periodic reference (every candidate
+    has the same multiset of squares: the winner is decided by the rounding order), flat ties,
+    NaN / inf pixels, and frame sizes narrower / not a multiple of a workgroup round."""
+    rng = np.random.default_rng(sr * 7 + np.dtype(dtype).itemsize)
+    for H, W in ((16, 16), (8, 224), (72, 264), (136, 120), (48, 8)):
+        a = rng.normal(128, 50, (H + 40, W + 40)).astype(dtype)
+        ref, cur = a[:H, :W].copy(), (a[3:H + 3, 5:W + 5] + rng.normal(0, 0.3, (H, W))).astype(dtype)
+        tile = rng.normal(100, 30, (8, 8))
+        per = np.tile(tile, (H // 8 + 1, W // 8 + 1))[:H, :W].astype(dtype)
+        cur_p = np.roll(per, (1, 2), axis=(0, 1)) + dtype(0.37)
+        nan_ref = ref.copy()
+        nan_ref[::9, ::11] = np.nan
+        nan_ref[5, :] = np.inf
+        flat = np.full((H, W), 3.25, dtype)
+        for r_, c_, what in ((ref, cur, "shift"), (per, cur_p, "periodic"), (nan_ref, cur, "nan/inf"),
+                             (flat, flat, "flat"), (cur, np.full((H, W), np.nan, dtype), "all-nan")):
+            mv = MotionCompensator(sr).compute_motion_vector(r_, c_)
+            assert_bits(mv, c_motion_vectors(r_, c_, sr), f"{np.dtype(dtype).name} sr={sr} {H}x{W} {what}")
+
+
+def test_me_float_search_device_frames_and_1080p():
+    """Several frame pairs in one device call (rounds over frames), and a full non-integer
+    1080p float64 pair at sr = 16 checked on sampled block rows."""
+    import torch
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(1920)
+    lo = rng.normal(120, 40, (290, 500))
+    big = np.kron(lo, np.ones((4, 4)))[:1120, :1960] * (219 / 255) + 16.0 + rng.normal(0, 1.5, (1120, 1960))
+    fr = np.stack([big[k:k + 1080, 2 * k:2 * k + 1920] for k in range(3)])
+    t = torch.from_numpy(np.ascontiguousarray(fr)).cuda()
+    mv = torch.empty((2, 135, 240), dtype=torch.int64, device="cuda")
+    D.motion_estimate(t[:-1].contiguous(), t[1:].contiguous(), 16, mv)
+    got = mv.cpu().numpy()
+    for p in range(2):
+        for rows in ((0, 3), (67, 70), (132, 135)):
+            want = c_motion_vectors(fr[p], fr[p + 1], 16, rows=rows)[..., 0]
+            assert_bits(got[p, rows[0]:rows[1]], want, f"pair {p} rows {rows}")
