@@ -5,8 +5,9 @@ of 256 synthetic 3840x2160 luma frames per GPU, resident in HBM, through the fus
 patch -> DCT-II -> quantise kernel (reference-equivalent output: [F,270,480,3,64] int32, the
 C = 1 -> 3-plane broadcast of patchquant.py:59).  One step = one pass over the batch.
 `roofline` prices that kernel against HBM (13 B/px algorithmic, HIP events on its stream;
-`traffic` = the rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE record of this very libivc.so build, or
-null), `cpu_baseline` times the reference's algorithm (oracle) on one host core,
+`traffic` = HBM bytes per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes run as
+child processes at the end of this run (1 rank; else the committed record of this very
+libivc.so build, or null), `cpu_baseline` times the reference's algorithm (oracle) on one host core,
 `cpu_baseline_multicore` on every core the box grants this process.
 
 Also reported from the same run (each with its own timing; none of them is `value`):
@@ -223,6 +224,80 @@ def lib_sha256():
     from ivclab_amd import _native as N
     with open(N.LIB_PATH, "rb") as fh:
         return hashlib.sha256(fh.read()).hexdigest()
+
+
+# ---------------------------------------------------------------- HBM traffic (PMC) -----
+INTRA_KERNEL_MATCH = "fused_encode_kernel<unsigned char, double, double, 1,"
+
+
+def pmc_child(args):
+    """--pmc-child: the headline kernel alone on the bench workload (same frames, same output
+    buffer shape), launched twice; run under `rocprofv3 --pmc <counter>` by pmc_traffic."""
+    import ivclab_amd.device as D
+    from ivclab_amd import PatchQuant
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    F, H, W = args.frames, args.height, args.width
+    frames = intra_frames(F, H, W, seed=3, dev=dev).view(F, H, W, 1)
+    out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+    table = PatchQuant(1.0).get_quantization_table()
+    for _ in range(2):
+        D.intra_encode(frames, table, out, zigzag=args.zigzag)
+    torch.cuda.synchronize()
+
+
+def _pmc_counter_mean(root, counter, match):
+    """Mean per-dispatch value of `counter` over the dispatches of kernels whose name contains
+    `match`, from a rocprofv3 --pmc CSV output directory."""
+    import csv
+    import glob
+    per = {}
+    for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if match in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+                    per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    return (sum(per.values()) / len(per), len(per)) if per else (None, 0)
+
+
+def pmc_traffic(args, timeout_s=150):
+    """HBM bytes per launch of the headline kernel, measured on this box during the bench:
+    two child processes (`rocprofv3 --pmc FETCH_SIZE`, then `--pmc WRITE_SIZE`: they do not
+    fit one pass) each running --pmc-child under its own kill timer.  Corrections as
+    MI355X_MICROARCH.md's HBM/rocprofv3 section prescribes: the counters are KiB; on gfx950
+    FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read, so it is doubled;
+    WRITE_SIZE is exact for 16 B/lane stores.  Returns (bytes or None, detail dict)."""
+    import shutil
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, {"error": "rocprofv3 not found"}
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--frames", str(args.frames),
+             "--height", str(args.height), "--width", str(args.width)] + (["--zigzag"] if args.zigzag else [])
+    env = dict(os.environ, TMPDIR="/tmp")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    vals, detail = {}, {}
+    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix="ivc_pmc_", dir="/tmp")
+        try:
+            r = subprocess.run(["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", ctr,
+                                "--output-format", "csv", "-d", d, "-o", "run", "--"] + child,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, env=env)
+            if r.returncode != 0:
+                return None, {"error": f"{ctr} pass exit {r.returncode}",
+                              "stderr_tail": r.stderr.decode(errors="replace")[-300:]}
+            v, n = _pmc_counter_mean(d, ctr, INTRA_KERNEL_MATCH)
+            if v is None:
+                return None, {"error": f"{ctr}: no dispatch of the kernel in the PMC output"}
+            vals[ctr], detail[f"{ctr}_dispatches"] = v, n
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    fetch = 2.0 * vals["FETCH_SIZE"] * 1024
+    write = vals["WRITE_SIZE"] * 1024
+    detail.update({"fetch_bytes": round(fetch), "write_bytes": round(write),
+                   "correction": "FETCH_SIZE x 2 (gfx950 wide-read half count), WRITE_SIZE as is; KiB -> B"})
+    return fetch + write, detail
 
 
 # ---------------------------------------------------------------- CPU baselines ---------
@@ -491,7 +566,7 @@ def leg_inter(args, dist, rank, world, dev, table, result, verify):
         "ms_per_step": round(iwall / args.inter_steps * 1e3, 3),
         "config": {"workload": f"cfg4: {Fi} frames 1920x1080 u8 luma per GPU, sr={sr}, "
                                "ME against the previous source frame (open loop)"},
-        "roofline": {"bound": "valu (v_dot4_u32_u8)", "kernel": "me_s2_kernel + me_fast_u8_kernel<16>",
+        "roofline": {"bound": "valu (v_dot4_u32_u8)", "kernel": "me_s2_kernel<true> + me_tile16_kernel",
                      "kernel_ms": round(me_ms, 4),
                      "achieved": round(dot4 / (me_ms * 1e-3) / 1e12, 2), "peak": round(DOT4_PEAK_T, 2),
                      "unit": "T dot4 lane-ops/s", "frac": round(dot4 / (me_ms * 1e-3) / 1e12 / DOT4_PEAK_T, 4),
@@ -734,6 +809,9 @@ def parse(argv=None):
     ap.add_argument("--no-sharded", action="store_true", help="skip the cfg5 8K leg")
     ap.add_argument("--no-cpu-pool", action="store_true", help="skip the multi-core CPU leg")
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle checks")
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the in-run rocprofv3 --pmc traffic passes (roofline.traffic)")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--sharded-frames", type=int, default=120)
     ap.add_argument("--sharded-height", type=int, default=4320)
     ap.add_argument("--sharded-width", type=int, default=7680)
@@ -744,6 +822,8 @@ def parse(argv=None):
                     help="frame pairs per inter_encode call in the cfg5 step; the histogram of "
                          "chunk k runs on a side stream while chunk k+1 is encoded (0: one call)")
     args = ap.parse_args(argv)
+    if args.pmc_child:
+        return args
     if not 0 <= args.sharded_hist_wg <= 16:
         ap.error("--sharded-hist-wg must be in [0, 16]")
     if args.gpus < 1:
@@ -753,6 +833,9 @@ def parse(argv=None):
 
 def main():
     args = parse()
+    if args.pmc_child:
+        pmc_child(args)
+        return
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # start the ranks ourselves (nothing has touched the GPU yet) and pass their status on
         sys.exit(subprocess.call(launcher_cmd(args.gpus, sys.argv[1:], free_port())))
@@ -815,6 +898,19 @@ def main():
                           "core the box grants: affinity, capped by the cgroup quota): intra on "
                           "whole 4K frames (~4 s), the ME loop on one 16-row stripe of a 1080p "
                           "pair per worker, extrapolated per valid candidate"}
+
+    # ---- HBM traffic of the headline kernel, from PMC counters on this box --------------------
+    if world == 1 and not args.no_pmc and not args.no_intra:
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        tb, tdet = pmc_traffic(args)
+        rl = result["roofline"]
+        if tb is not None:
+            rl["traffic"] = round(tb)
+            rl["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE passes of this "
+                                    "kernel on this box during this run (child processes)")
+            rl["traffic_vs_algorithmic"] = round(tb / rl["algorithmic_bytes_per_launch"], 4)
+        rl["traffic_detail"] = tdet
 
     if verify is not None:
         fails = verify["failures"]

@@ -540,6 +540,31 @@ def test_me_exact_u8_fast_paths(sr, shape):
         assert_bits(mv, want.astype(np.int64), f"exact u8 sr={sr} {shape}")
 
 
+@pytest.mark.parametrize("sr", [4, 8, 16])
+@pytest.mark.parametrize("shape", [(88, 200), (40, 136), (24, 48)])
+def test_me_exact_u8_extremes_multi_frame(sr, shape):
+    """Several frame pairs in one call (the tiled sr=16 kernel's tiles cross frames), with
+    extreme contrast: binary 0/255 content (SSDs up to 64 * 255^2, the top of the key range),
+    all-255 against all-0 (every candidate ties at the maximum), and mixed — against the C
+    oracle, frame by frame."""
+    import ivclab_amd._native as N
+    rng = np.random.default_rng(sr * 7 + shape[1])
+    H, W = shape
+    binary = (rng.integers(0, 2, (H + 40, W + 40)) * 255).astype(np.uint8)
+    refs = [binary[:H, :W], np.full((H, W), 255, np.uint8), rng.integers(0, 256, (H, W), dtype=np.uint8),
+            binary[5:H + 5, 2:W + 2]]
+    curs = [binary[2:H + 2, 6:W + 6], np.zeros((H, W), np.uint8), np.full((H, W), 255, np.uint8),
+            np.flipud(binary[:H, :W])]
+    ref = np.ascontiguousarray(np.stack(refs))
+    cur = np.ascontiguousarray(np.stack(curs))
+    F = ref.shape[0]
+    mv = np.empty((F, H // 8, W // 8, 1), np.int64)
+    N.check(N.lib().ivc_motion_estimate(N.ptr(ref), N.ptr(cur), 1, F, H, W, sr, N.ME_EXACT_U8, N.ptr(mv)))
+    for f in range(F):
+        want = c_motion_vectors(ref[f].astype(np.float64), cur[f].astype(np.float64), sr)
+        assert_bits(mv[f], want.astype(np.int64), f"extremes sr={sr} {shape} frame {f}")
+
+
 def test_me_exact_u8_full_hd_vs_c_oracle():
     """A full 1080p pair at sr=16 (the bench configuration), checked on sampled block rows
     (top, middle, bottom) against the C oracle."""
