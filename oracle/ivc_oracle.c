@@ -27,7 +27,7 @@ enum { U8 = 1, I8, U16, I16, U32, I32, U64, I64, F32, F64 };
     for (int u = 0; u < 8; ++u)                                                         \
       for (int v = 0; v < 8; ++v) {                                                     \
         UT d = (UT)((UT)cur[(y + u) * W + x + v] - (UT)ref[(ry + u) * W + rx + v]);     \
-        UT q = (UT)(d * d);                                                             \
+        UT q = (UT)((uint64_t)d * (uint64_t)d); /* no int promotion: d*d overflows int */ \
         s = (ACC)((uint64_t)s + (uint64_t)(ACC)(T)q);                                   \
       }                                                                                 \
     return s;                                                                           \
