@@ -1,0 +1,41 @@
+"""Profiling child: the cfg3 entropy stages alone — ZeroRunCoder.encode of the zig-zag
+coefficients (zw_count / scan / zw_emit) and the fused pixels -> symbols path (fused encoder
+OUT_COUNT / scan / OUT_SYMBOLS), once each on 256 (SYM_FRAMES) 4K frames.  Run under
+`rocprofv3 --pmc ...`."""
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+import ivclab_amd.device as D  # noqa: E402
+from ivclab_amd import PatchQuant  # noqa: E402
+
+
+def main():
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    F = int(os.environ.get("SYM_FRAMES", "256"))
+    H, W = 2160, 3840
+    frames = bench.intra_frames(F, H, W, seed=3, dev=dev).view(F, H, W, 1)
+    table = PatchQuant(1.0).get_quantization_table()
+    out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+    D.intra_encode(frames, table, out, zigzag=True)
+    nblk = out.numel() // 64
+    offs = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
+    probe = torch.empty(1, dtype=torch.int32, device=dev)
+    D.zerorun_encode(out.view(nblk, 64), offs, probe)
+    nsym = int(offs[-1].item())
+    sym = torch.empty(nsym, dtype=torch.int32, device=dev)
+    D.zerorun_encode(out.view(nblk, 64), offs, sym)
+    nsd = torch.zeros(1, dtype=torch.int64, device=dev)
+    D.intra_symbols(frames, table, sym, nsd)
+    torch.cuda.synchronize()
+    print("sym_pmc_child done", nsym)
+
+
+if __name__ == "__main__":
+    main()
