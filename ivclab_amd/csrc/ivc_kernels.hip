@@ -1056,6 +1056,11 @@ static double pace_start_rate() {
 // Folds every completed measurement, oldest first (caller holds g_pace_mu).
 static void pace_harvest(PaceState& P) {
   while (P.count > 0) {
+    if (P.rate <= 0) {            // pacing switched off since: drop the measurements
+      P.head = (P.head + P.count) % PACE_RING;
+      P.count = 0;
+      break;
+    }
     PaceSlot& S = P.ring[P.head];
     if (hipEventQuery(S.done) != hipSuccess) break;
     uint64_t late = 0;

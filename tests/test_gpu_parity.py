@@ -670,7 +670,7 @@ def test_zerorun_device_api_and_capacity():
     assert np.array_equal(dec.cpu().numpy(), x)
 
 
-@pytest.mark.parametrize("nblk", [1, 15, 16, 17, 1023, 1024 * 16 + 5, 300001])
+@pytest.mark.parametrize("nblk", [1, 15, 16, 17, 1023, 1024 * 16 + 5, 300001, 1500001])
 def test_zerorun_device_wide_and_general(nblk):
     """The device encoder's wide path (dense, 16-B aligned 64-coefficient rows: 16 blocks per
     wave-iteration) against the oracle and an independent per-block count: ends that are not
