@@ -419,11 +419,12 @@ __device__ __forceinline__ uint32_t pace_until(uint64_t t256, uint32_t slack) {
 
 // pace block: [0] start time (ticks), [1..8] late-slot counters (sharded: one atomic word
 // saturates near 90 updates/us)
-constexpr int PACE_SHARDS = 8;
+constexpr int PACE_SHARDS = 8, PACE_WORDS = 1 + PACE_SHARDS;
 __global__ void pace_stamp_kernel(uint64_t* blk, uint32_t lead) {
   blk[0] = __builtin_amdgcn_s_memrealtime() + lead;
-  for (int i = 1; i <= PACE_SHARDS; ++i) blk[i] = 0;
+  for (int i = 1; i < PACE_WORDS; ++i) blk[i] = 0;
 }
+
 
 // A group = 8 horizontally adjacent blocks of one block row (one wave-step of compute and
 // one 6 KiB store); a load tile = NG consecutive groups, whose 8 image rows the wave loads
@@ -1010,12 +1011,17 @@ static unsigned resident_grid(K kernel, int64_t work_groups_needed) {
 // copied to pinned memory and its duration from two events), and completed measurements are
 // folded in launch order when a later launch is set up, or when the statistics are read:
 //  * late slots above PACE_LATE_HI of the launch's slots: the schedule outran the device.
-//    The rate drops to the lower of 98% of itself and 98.5% of what that launch actually
-//    moved (bytes / duration) — one measured launch brings a start rate that is far too fast
-//    back under the device's pace — and the launch's rate becomes the "too fast" mark;
-//  * otherwise the rate creeps up (+1.5% per launch while under 97% of the mark, +0.3%
-//    nearer it), never past 99% of the mark, which itself rises 0.2% per good launch so a
-//    transient cannot cap the rate for good.
+//    The rate drops to the lower of 98% of itself and 1.1x what that launch actually moved
+//    (bytes / duration; over the pace the sweep runs ~10% under it) — one measured launch
+//    brings a start rate that is far too fast back near the device's pace — and the launch's
+//    rate becomes the "too fast" mark;
+//  * otherwise the rate creeps up (+1.5% per launch while under 96% of the mark, +0.3%
+//    nearer it), never past 98% of the mark (the edge is sharp and bimodal: launches at
+//    99% of a failed rate still fail half the time), which itself rises 0.1% per good launch
+//    so a transient cannot cap the rate for good;
+//  * the first measured launch only records (it writes fresh output pages and runs slow).
+//  Fixed-rate sweeps (IVC_PACE_FIXED, two boxes): good launches hold the schedule to within
+//  ~35 us; the edge sat at 5.9 and 6.1-6.2 TB/s.
 // IVC_PACE_GBPS / ivc_set_store_pace set the starting rate (0 disables pacing).
 static std::mutex g_pace_mu;
 static double g_pace_start = -1.0;
@@ -1039,6 +1045,7 @@ struct PaceState {
   int head = 0, count = 0;        // oldest in-flight measurement, number in flight
   int armed = -1;                 // slot of the launch being set up
   double rate = 0, too_fast = 1e30, last_late = -1;
+  bool seen_first = false;        // the process's first measured launch (not adapted on)
   PaceStats st;
 };
 // per device and per encoder (0: image source, 1: inter residual source)
@@ -1051,6 +1058,13 @@ static double pace_start_rate() {
     if (!(g_pace_start >= 0)) g_pace_start = 0;
   }
   return g_pace_start;
+}
+
+// IVC_PACE_FIXED (set): keep the rate where ivc_set_store_pace / IVC_PACE_GBPS put it and
+// only record the launches' measurements (rate sweeps, tools/ab/ab_intra.py --pace).
+static bool pace_fixed() {
+  static const bool f = getenv("IVC_PACE_FIXED") != nullptr;
+  return f;
 }
 
 // Folds every completed measurement, oldest first (caller holds g_pace_mu).
@@ -1074,16 +1088,24 @@ static void pace_harvest(PaceState& P) {
     P.st.sum_late += f;
     P.st.max_late = std::max(P.st.max_late, f);
     P.st.sum_gbps += gbps;
-    if (f > PACE_LATE_HI) {
+    const bool first = P.st.measured == 1 && !P.seen_first;   // fresh output pages: slow
+    P.seen_first = true;
+    if (pace_fixed()) {
+      if (f > PACE_LATE_HI) P.st.over += 1;
+    } else if (first) {
+      if (f > PACE_LATE_HI) P.st.over += 1;
+    } else if (f > PACE_LATE_HI) {
       P.st.over += 1;
       P.too_fast = std::min(P.too_fast, S.rate);
+      // a launch over the device's pace runs ~10% under it (late waves store out of address
+      // order), so 1.1x what it moved is about the pace; never above 98% of the failed rate
       double r = P.rate * 0.98;
-      if (gbps > 0) r = std::min(r, 0.985 * gbps);
+      if (gbps > 0) r = std::min(r, 1.1 * gbps);
       P.rate = std::max(r, 100.0);
     } else {
-      P.too_fast *= 1.002;
-      const double cap = std::min(PACE_MAX_GBPS, 0.99 * P.too_fast);
-      const double step = P.rate < 0.97 * P.too_fast ? 1.015 : 1.003;
+      P.too_fast *= 1.001;
+      const double cap = std::min(PACE_MAX_GBPS, 0.98 * P.too_fast);
+      const double step = P.rate < 0.96 * P.too_fast ? 1.015 : 1.003;
       P.rate = std::max(std::min(P.rate * step, cap), P.rate);
     }
     P.head = (P.head + 1) % PACE_RING;
@@ -1150,7 +1172,7 @@ void set_store_pace_gbps(double gbps) {
 }
 
 static bool pace_alloc(PaceState& P) {
-  if (hipMalloc((void**)&P.blk, 8 * (1 + PACE_SHARDS)) != hipSuccess) {
+  if (hipMalloc((void**)&P.blk, 8 * PACE_WORDS) != hipSuccess) {
     P.blk = nullptr;
     return false;
   }
