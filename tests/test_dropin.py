@@ -114,3 +114,85 @@ print(json.dumps({{"mean_energy": float(np.mean(transformed ** 2)),
     assert abs(got["mse"] - want["mse"]) <= 5                            # ch3.py:47
     for k in ("mean_energy", "mean_q2", "mse", "psnr"):
         assert got[k] == float(want[k]), k
+
+
+# exercises/ch3/ex1.py's rate-distortion loop (its quantisation scales, Huffman trained on a
+# small training image with is_source_rgb=False, the large image coded and decoded), through
+# the drop-in names on synthetic stand-ins for the absent data/lena.tif / lena_small.tif
+RD_SCALES = [0.05, 0.1, 0.15, 0.2, 0.3]
+RD_CODE = """
+import json
+import numpy as np
+import ivclab_amd; ivclab_amd.install_as_ivclab()
+from ivclab.image import IntraCodec
+from ivclab.utils import calc_psnr
+rng = np.random.default_rng(31)
+yy, xx = np.mgrid[0:256, 0:384]
+base = 128 + 60 * np.sin(xx / 23.0) * np.cos(yy / 17.0) + 0.2 * (xx - yy)
+lena = np.stack([base + 25 * np.sin(yy / (7.0 + 3 * c)) for c in range(3)], axis=-1)
+lena = np.clip(lena + rng.normal(0, 6, lena.shape), 0, 255).astype(np.uint8)
+lena_small = np.ascontiguousarray(lena[::2, ::2])
+rows = []
+for q in %r:
+    codec = IntraCodec(quantization_scale=q)
+    codec.train_huffman_from_image(lena_small, is_source_rgb=False)
+    rec, bitstream, bitsize, bpp = codec.encode_decode(lena, return_bpp=True, is_source_rgb=False)
+    syms = codec.image2symbols(lena, is_source_rgb=False)
+    np.save(f"{OUT}/rec_{q}.npy", rec)
+    np.save(f"{OUT}/sym_{q}.npy", np.asarray(syms, np.int32))
+    np.save(f"{OUT}/len_{q}.npy", np.asarray(codec.huffman.encoder_codebook, np.int64))
+    np.save(f"{OUT}/pmf_{q}.npy", np.asarray(codec.huffman.probs, np.float64))
+    rows.append({"q": q, "psnr": float(calc_psnr(lena, rec)), "bits": int(bitsize), "bpp": float(bpp),
+                 "bounds": list(codec.bounds)})
+np.save(f"{OUT}/lena.npy", lena)
+print(json.dumps(rows))
+"""
+
+
+@pytest.mark.gpu
+def test_exercise_ch3_rd_curve(tmp_path):
+    """exercises/ch3/ex1.py's RD loop through the drop-in: every reconstruction equals the
+    oracle chain (patch -> DCT -> quantise -> zig-zag -> zero-run -> decode -> dequantise ->
+    IDCT -> unpatch -> ycbcr2rgb) bit for bit, so every PSNR is the reference's; the symbol streams equal
+    the oracle's.  Bitrates (bitstreams are not pinned: constriction's tie-breaking is
+    absent): the bit count is the sum of the coder's code lengths over the stream, the
+    lengths are a complete prefix code (Kraft sum 1) within the Huffman bound on the trained
+    pmf (mean length < H(pmf) + 1), and no prefix code spends fewer bits than the stream's
+    empirical entropy.  The bitrate falls as the scale grows."""
+    import json
+    sys.path.insert(0, ROOT)
+    from oracle import ivc_oracle as O
+    code = f"OUT = {str(tmp_path)!r}\n" + RD_CODE % (RD_SCALES,)
+    rows = json.loads(run_py(code).strip().splitlines()[-1])
+    lena = np.load(tmp_path / "lena.npy")
+    H, W, _ = lena.shape
+    for r in rows:
+        q = r["q"]
+        zz = O.intra_encode(lena, q, zigzag=True)
+        want_sym = O.zerorun_encode_fast(zz.reshape(-1, 64))
+        got_sym = np.load(tmp_path / f"sym_{q}.npy")
+        assert np.array_equal(got_sym, want_sym), f"symbols q={q}"
+        dec = O.zerorun_decode(want_sym, (H // 8, W // 8, 3))
+        # symbols2image of a 3-D shape ends in ycbcr2rgb, even for is_source_rgb=False input
+        # (intracodec.py:140-146, the reference's behaviour)
+        want_rec = O.ycbcr2rgb(O.unpatch(O.intra_decode(dec, q, unzigzag=True)))
+        rec = np.load(tmp_path / f"rec_{q}.npy")
+        assert rec.dtype == want_rec.dtype and rec.shape == want_rec.shape
+        assert rec.tobytes() == want_rec.tobytes(), f"reconstruction q={q}"
+        assert r["psnr"] == float(20 * np.log10(255 / np.sqrt(np.mean((lena.astype(np.float64) - want_rec) ** 2))))
+        # the trained code (intracodec.py:149-166: pmf over [min-20, max+21), smoothed)
+        lo = r["bounds"][0]
+        ln = np.load(tmp_path / f"len_{q}.npy")
+        pmf = np.load(tmp_path / f"pmf_{q}.npy")
+        assert r["bits"] == int(ln[want_sym - lo].sum())
+        assert abs(np.sum(2.0 ** -ln.astype(np.float64)) - 1.0) < 1e-12
+        h = -np.sum(pmf * np.log2(pmf))
+        assert np.sum(pmf * ln) < h + 1
+        e = np.bincount(want_sym - want_sym.min()).astype(np.float64)
+        e = e[e > 0] / len(want_sym)
+        assert r["bits"] >= len(want_sym) * -np.sum(e * np.log2(e)) - 1e-6
+        assert r["bpp"] == r["bits"] / (H * W)
+    # coarser quantisation: fewer bits (PSNR is not monotone here: the reference decodes a 3-D
+    # shape through ycbcr2rgb although this image was coded as YCbCr, with clipping)
+    bpp = [r["bpp"] for r in rows]
+    assert all(a > b for a, b in zip(bpp, bpp[1:])), rows
