@@ -458,6 +458,9 @@ static unsigned me_fast_grid(const void* kernel, int64_t wgs) {
 #ifndef IVC_ME_TILE
 #define IVC_ME_TILE 1                      // SR = 16: tiled search (me_tile16_kernel)
 #endif
+#ifndef IVC_ME_ABL
+#define IVC_ME_ABL 0                       // diagnostic builds: bit mask of skipped phases
+#endif
 #ifndef IVC_ME_TILE_PREFETCH
 #define IVC_ME_TILE_PREFETCH 0
 #endif
@@ -807,7 +810,7 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
 #pragma unroll
     for (int r = 0; r < IPT; ++r) {
       const int i = tid + 256 * r;
-      if (i < ITEMS) {
+      if (i < ITEMS && !(IVC_ME_ABL & 4)) {
         const int row = i / NPAIR, p = i - row * NPAIR;
         uint32_t* d = lds + row * PITCH + 2 * p;
         const uint32_t w0 = raw[r][0], w1 = raw[r][1], w2 = raw[r][2];
@@ -870,8 +873,13 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
 #pragma unroll
       for (int d = 0; d < DYT; ++d) {
         const int off = ((ry0 + d) * W + s * W4 + qb) * 4;
-        nsa[d] = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
-        nsb[d] = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 8, 0, 0);
+        if (IVC_ME_ABL & 2) {
+          nsa[d] = me_u32x2{(uint32_t)off, 0u};
+          nsb[d] = me_u32x2{0u, (uint32_t)off};
+        } else {
+          nsa[d] = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+          nsb[d] = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 8, 0, 0);
+        }
       }
       const uint32_t* const wb = cbase + 2 * j;
       // the 6 words of a row (5 used) are read one row ahead of their use, as three
@@ -884,9 +892,9 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
         v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y; v[4] = c.x; v[5] = c.y;
       };
       uint32_t v[6];
-      row_words(0, v);
+      if (!(IVC_ME_ABL & 1)) row_words(0, v);
 #pragma unroll
-      for (int rr = 0; rr < DYT + 7; ++rr) {
+      for (int rr = 0; rr < ((IVC_ME_ABL & 1) ? 0 : DYT + 7); ++rr) {
         uint32_t nv[6] = {0u, 0u, 0u, 0u, 0u, 0u};
         if (rr + 1 < DYT + 7) row_words(rr + 1, nv);
 #pragma unroll
@@ -927,12 +935,12 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
         bi = (uint32_t)((dy0 + (r >> 2)) * N + 4 * (m0 + (r & 3)) + s);
       }
       // lexicographic (K, raster index) minimum over the wave: first strict minimum
-      const uint32_t mk = wave_min_u32(bk);
-      const uint32_t mi = wave_min_u32(bk == mk ? bi : 0x7fffffffu);
+      const uint32_t mk = (IVC_ME_ABL & 8) ? bk : wave_min_u32(bk);
+      const uint32_t mi = (IVC_ME_ABL & 8) ? bi : wave_min_u32(bk == mk ? bi : 0x7fffffffu);
       if (lane == 0)
         mv[((int64_t)f * h + by) * w + bx] = mi == 0x7fffffffu ? (int64_t)SR * N + SR : (int64_t)mi;
     }
-    if (!IVC_ME_TILE_PREFETCH) {                           // fewer registers: 5 waves per SIMD
+    if (!IVC_ME_TILE_PREFETCH && !(IVC_ME_ABL & 16)) {     // fewer registers: 5 waves per SIMD
       const uint32_t nt = tile + gridDim.x;
       load_tile(nt, nt < ntiles, raw, craw);
     }
