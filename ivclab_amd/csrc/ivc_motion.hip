@@ -179,7 +179,13 @@ __global__ __launch_bounds__(256) void me_generic_kernel(const T* __restrict__ r
 // (SSD, raster index) minimum over its 2sr+1 threads: an LDS atomic minimum of the SSD bits
 // (non-negative doubles order like their bits), a barrier, then the minimum index among the
 // threads holding that SSD — the reference's first strict minimum.
-constexpr int FLT_WG = 512, FLT_DY = 11;
+#ifndef IVC_FLT_DY
+#define IVC_FLT_DY 11
+#endif
+#ifndef IVC_FLT_WGCU
+#define IVC_FLT_WGCU 1     // f64 workgroups per CU (2 needs <= 128 VGPRs: FLT_DY 6)
+#endif
+constexpr int FLT_WG = 512, FLT_DY = IVC_FLT_DY;
 
 template <typename T> struct FltBits;
 template <> struct FltBits<double> {
@@ -196,9 +202,13 @@ template <> struct FltBits<float> {
 // it) and clobbers memory (so no LDS load moves above it).
 template <typename T>
 __device__ __forceinline__ void flt_pin(T (&a)[FLT_DY]) {
-  static_assert(FLT_DY == 11, "flt_pin lists FLT_DY operands");
-  __asm__ volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
-                   "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]) :: "memory");
+  static_assert(FLT_DY == 11 || FLT_DY == 6, "flt_pin lists FLT_DY operands");
+  if constexpr (FLT_DY == 11)
+    __asm__ volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]),
+                     "+v"(a[6]), "+v"(a[7]), "+v"(a[8]), "+v"(a[9]), "+v"(a[10]) :: "memory");
+  else
+    __asm__ volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5])
+                     :: "memory");
 }
 
 // Round geometry: NBR blocks per round (2sr+1 threads each), capped so that the window, the
@@ -208,11 +218,14 @@ template <typename T, int SR> struct FltGeom {
   // WR window rows plus the rows a partial last dy run reads past them (zeros, never used)
   static constexpr int N = 2 * SR + 1, WR = 8 + 2 * SR;
   static constexpr int RUNS = (N + FLT_DY - 1) / FLT_DY, WRP = RUNS * FLT_DY + 7;
-  static constexpr int PER_NB = (WRP * 8 + 64) * (int)sizeof(T) + (int)sizeof(T) + 4;
+  // a block's 64 pixels at a pitch 16 B past 64 elements: the blocks a half-wave's 16-byte
+  // reads broadcast from then start on different banks
+  static constexpr int CBP = 64 + 16 / (int)sizeof(T);
+  static constexpr int PER_NB = (WRP * 8 + CBP) * (int)sizeof(T) + (int)sizeof(T) + 4;
   static constexpr int NB_LDS = (FLT_LDS - WRP * 2 * SR * (int)sizeof(T)) / PER_NB;
   static constexpr int NBR = FLT_WG / N < NB_LDS ? FLT_WG / N : NB_LDS;
   static constexpr int WC = NBR * 8 + 2 * SR;
-  static constexpr size_t LDS = ((size_t)WRP * WC + (size_t)NBR * 64) * sizeof(T) +
+  static constexpr size_t LDS = ((size_t)WRP * WC + (size_t)NBR * CBP) * sizeof(T) +
                                 (size_t)NBR * (sizeof(T) + 4);
   static_assert(NBR >= 1 && LDS <= (size_t)FLT_LDS, "round does not fit the LDS budget");
 };
@@ -228,8 +241,8 @@ __global__ __launch_bounds__(FLT_WG, sizeof(T) == 8 ? 2 : 4) void me_flt_kernel(
   constexpr int sr = SR, n = G::N, nbr = G::NBR, WR = G::WR, WC = G::WC, WRP = G::WRP;
   const int h = H / 8, w = W / 8;
   T* win = reinterpret_cast<T*>(flt_smem);                // [WRP][WC]
-  T* cb = win + WRP * WC;                                 // [nbr][v][u]
-  U* kmin = reinterpret_cast<U*>(cb + nbr * 64);          // [nbr]
+  T* cb = win + WRP * WC;                                 // [nbr][v][u], pitch CBP
+  U* kmin = reinterpret_cast<U*>(cb + nbr * G::CBP);      // [nbr]
   unsigned* imin = reinterpret_cast<unsigned*>(kmin + nbr);
   const int segs = (w + nbr - 1) / nbr;
   const int64_t rounds = nframes * h * segs;
@@ -249,7 +262,7 @@ __global__ __launch_bounds__(FLT_WG, sizeof(T) == 8 ? 2 : 4) void me_flt_kernel(
     }
     for (int i = tid; i < nb * 64; i += FLT_WG) {
       const int b = i >> 6, u = (i >> 3) & 7, v = i & 7;
-      cb[b * 64 + v * 8 + u] = cf[(int64_t)(8 * by + u) * W + 8 * (bx0 + b) + v];
+      cb[b * G::CBP + v * 8 + u] = cf[(int64_t)(8 * by + u) * W + 8 * (bx0 + b) + v];
     }
     for (int i = tid; i < nb; i += FLT_WG) {
       kmin[i] = ~(U)0;
@@ -260,7 +273,7 @@ __global__ __launch_bounds__(FLT_WG, sizeof(T) == 8 ? 2 : 4) void me_flt_kernel(
     int bidx = -1;
     const int rx = 8 * (bx0 + sb) + se - sr;
     if (sb < nb && rx >= 0 && rx + 8 <= W) {
-      const T* cblk = cb + sb * 64;
+      const T* cblk = cb + sb * G::CBP;
 #pragma unroll 1
       for (int dy0 = 0; dy0 < n; dy0 += FLT_DY) {
         T ta[FLT_DY], tb[FLT_DY], tc[FLT_DY];
@@ -329,7 +342,7 @@ static void launch_me_flt_sr(const T* ref, const T* cur, int64_t nframes, int64_
   const int64_t rounds = nframes * h * ((w + G::NBR - 1) / G::NBR);
   const size_t lds = G::LDS;
   // f64: 144 VGPRs, one 512-thread workgroup per CU; f32: two (88 VGPRs, LDS permitting)
-  const unsigned grid = me_grid(rounds, 1, sizeof(T) == 4 && lds * 2 <= 160 * 1024 ? 2 : 1);
+  const unsigned grid = me_grid(rounds, 1, sizeof(T) == 4 && lds * 2 <= 160 * 1024 ? 2 : IVC_FLT_WGCU);
   me_flt_kernel<T, SR><<<grid, FLT_WG, lds, s>>>(ref, cur, nframes, (int)H, (int)W, mv);
 }
 
