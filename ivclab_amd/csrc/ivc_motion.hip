@@ -971,7 +971,8 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
   me_generic_kernel<T, M><<<grid, 256, 0, s>>>((const T*)ref, (const T*)cur, nframes, h, w, sr, mv)
   if (mode == IVC_ME_EXACT_U8) {
     if (dtype != IVC_U8) return hipErrorInvalidValue;
-    if (sr == 4 || sr == 8 || sr == 16) {
+    // the dot4 searches address a frame's S2 plane (4 B per pixel) with 32-bit buffer offsets
+    if ((sr == 4 || sr == 8 || sr == 16) && H * W * 4 < ((int64_t)1 << 31)) {
       // Frame pairs go in chunks of about IVC_ME_CHUNK_BYTES of S2 (one int32 per reference
       // pixel, stream-ordered scratch; at least one frame): a chunk the size of the 256 MB
       // Infinity Cache is still cache-resident when the search reads it right after the
