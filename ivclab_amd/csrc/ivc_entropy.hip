@@ -290,17 +290,21 @@ __device__ __forceinline__ zv4 zw_load(const int32_t* src, int64_t nblk, int64_t
   return __builtin_nontemporal_load(reinterpret_cast<const zv4*>(src + blk * 64) + (lane & 15));
 }
 
+#ifndef IVC_ZW_COUNT_GROUPS
+#define IVC_ZW_COUNT_GROUPS 4   // 16-block groups per wave-iteration of the count pass (4: -2%)
+#endif
 __global__ __launch_bounds__(256) void zw_count_kernel(const int32_t* __restrict__ src, int64_t nblk,
                                                        int32_t* __restrict__ counts) {
+  constexpr int NGR = IVC_ZW_COUNT_GROUPS;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t b0 = wave * ZW_BLK; b0 < nblk; b0 += nw * ZW_BLK) {
-    zv4 x[ZW_LOADS];
+  for (int64_t b0 = wave * ZW_BLK * NGR; b0 < nblk; b0 += nw * ZW_BLK * NGR) {
+    zv4 x[NGR * ZW_LOADS];
 #pragma unroll
-    for (int u = 0; u < ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
+    for (int u = 0; u < NGR * ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
 #pragma unroll
-    for (int u = 0; u < ZW_LOADS; ++u) {
+    for (int u = 0; u < NGR * ZW_LOADS; ++u) {
       const ZwMask z = zw_mask(x[u], lane);
       const int64_t blk = b0 + 4 * u + (lane >> 4);
       if ((lane & 15) == 0 && blk < nblk) counts[blk] = z.cnt;
@@ -375,7 +379,7 @@ hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, 
                                   int32_t* counts, int64_t* agg, int64_t* off, hipStream_t s) {
   if (nblk <= 0) return hipMemsetAsync(off, 0, sizeof(int64_t), s);
   if (zw_ok(src, stride, B))
-    zw_count_kernel<<<zw_grid(nblk, 8), 256, 0, s>>>(src, nblk, counts);
+    zw_count_kernel<<<zw_grid((nblk + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(src, nblk, counts);
   else
     zr_count_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, counts);
   return device_scan<int64_t>(nblk, CountGen{counts}, SumI64{}, OffsetSink{off, nblk}, agg, s);
