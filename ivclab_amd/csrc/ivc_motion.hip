@@ -854,6 +854,9 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
 #pragma unroll
     for (int d = 0; d < DYT; ++d)
       vy[d] = dy0 + d < N && ry0 + d >= 0 && ry0 + d + 8 <= H;
+    // a lane's S2 quad of block j + 1 is 2 words past block j's: its first pair is block j's
+    // second, carried over (one 8-byte load per dy after the wave's first block)
+    me_u32x2 nsa[DYT], nsb[DYT];
 #pragma unroll 1
     for (int jj = 0; jj < WPT; ++jj) {
       const int j = wave * WPT + jj;
@@ -882,7 +885,6 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
       // the block's -32 S2 words, issued before the search so their latency (HBM when the
       // chunk's S2 outgrows the caches, 8K) hides behind it
       const int qb = 2 * bx - SR / 4 + m0;                 // s-plane column of k = 0
-      me_u32x2 nsa[DYT], nsb[DYT];
 #pragma unroll
       for (int d = 0; d < DYT; ++d) {
         const int off = ((ry0 + d) * W + s * W4 + qb) * 4;
@@ -890,7 +892,7 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
           nsa[d] = me_u32x2{(uint32_t)off, 0u};
           nsb[d] = me_u32x2{0u, (uint32_t)off};
         } else {
-          nsa[d] = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+          nsa[d] = jj == 0 ? __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0) : nsb[d];
           nsb[d] = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 8, 0, 0);
         }
       }
