@@ -951,7 +951,12 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
       }
       // lexicographic (K, raster index) minimum over the wave: first strict minimum
       const uint32_t mk = (IVC_ME_ABL & 8) ? bk : wave_min_u32(bk);
-      const uint32_t mi = (IVC_ME_ABL & 8) ? bi : wave_min_u32(bk == mk ? bi : 0x7fffffffu);
+      // ties on the minimum K are rare outside flat content: one lane holding it is the answer
+      const uint64_t holders = __ballot(bk == mk);
+      const uint32_t mi = (IVC_ME_ABL & 8) ? bi
+                          : __builtin_popcountll(holders) == 1
+                              ? (uint32_t)__builtin_amdgcn_readlane((int)bi, __builtin_ctzll(holders))
+                              : wave_min_u32(bk == mk ? bi : 0x7fffffffu);
       if (lane == 0)
         mv[((int64_t)f * h + by) * w + bx] = mi == 0x7fffffffu ? (int64_t)SR * N + SR : (int64_t)mi;
     }
