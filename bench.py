@@ -900,7 +900,10 @@ def main():
                           "pair per worker, extrapolated per valid candidate"}
 
     # ---- HBM traffic of the headline kernel, from PMC counters on this box --------------------
-    if world == 1 and not args.no_pmc and not args.no_intra:
+    # under a profiler already (rocprofv3 sets ROCPROF_* for its tool library) a nested
+    # rocprofv3 child would inherit the profiler and re-exec an initialised process: skip
+    under_profiler = any(k.startswith("ROCPROF_") for k in os.environ)
+    if world == 1 and not args.no_pmc and not args.no_intra and not under_profiler:
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
         tb, tdet = pmc_traffic(args)

@@ -631,20 +631,18 @@ int ivc_zerorun_encode_dev(const int32_t* src, int64_t nblk, int32_t row_stride,
   TRY(check_zr(nblk, row_stride, block_size));
   CHECK(capacity >= 0, IVC_E_ARG, "zerorun: capacity must be >= 0");
   hipStream_t s = (hipStream_t)stream;
-  int32_t* counts = nullptr;
-  int64_t* agg = nullptr;
+  void* scratch = nullptr;
   if (nblk > 0) {
-    hipError_t e = scratch_alloc((void**)&counts, (size_t)nblk * 4, s);
-    if (e == hipSuccess) e = scratch_alloc((void**)&agg, (size_t)scan_scratch_elems(nblk) * 8, s);
+    hipError_t e = scratch_alloc(&scratch, (size_t)zerorun_scratch_bytes(nblk), s);
     if (e != hipSuccess) return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
   }
-  int rc = dev_launch(launch_zerorun_offsets(src, nblk, row_stride, block_size, counts, agg, offsets, s),
+  int rc = dev_launch(launch_zerorun_offsets(src, nblk, row_stride, block_size, scratch, offsets, s),
                       "zerorun_encode");
   if (!rc)
-    rc = dev_launch(launch_zerorun_emit(src, nblk, row_stride, block_size, eob, offsets, out, capacity, s),
+    rc = dev_launch(launch_zerorun_emit(src, nblk, row_stride, block_size, eob, scratch, offsets, out,
+                                        capacity, s),
                     "zerorun_encode");
-  if (counts) (void)hipFreeAsync(counts, s);
-  if (agg) (void)hipFreeAsync(agg, s);
+  if (scratch) (void)hipFreeAsync(scratch, s);
   return rc;
 }
 
@@ -656,11 +654,10 @@ int ivc_zerorun_encode(const int32_t* src, int64_t nblk, int32_t row_stride, int
   Staging st;
   TRY(st.open());
   const int32_t* d_src = (const int32_t*)st.in(src, (size_t)nblk * row_stride * 4);
-  int32_t* counts = (int32_t*)st.alloc((size_t)nblk * 4);
-  int64_t* agg = (int64_t*)st.alloc((size_t)scan_scratch_elems(nblk) * 8);
+  void* scratch = st.alloc((size_t)zerorun_scratch_bytes(nblk));
   int64_t* off = (int64_t*)st.alloc((size_t)(nblk + 1) * 8);
   if (st.status) return st.status;
-  TRY(st.launched(launch_zerorun_offsets(d_src, nblk, row_stride, block_size, counts, agg, off,
+  TRY(st.launched(launch_zerorun_offsets(d_src, nblk, row_stride, block_size, scratch, off,
                                          st.ctx->stream), "zerorun_encode"));
   int64_t total = 0;
   TRY(st.out(&total, off + nblk, 8));
@@ -671,7 +668,7 @@ int ivc_zerorun_encode(const int32_t* src, int64_t nblk, int32_t row_stride, int
                                  " symbols, more than capacity " + std::to_string(capacity));
   int32_t* d_out = (int32_t*)st.alloc((size_t)total * 4);
   if (st.status) return st.status;
-  TRY(st.launched(launch_zerorun_emit(d_src, nblk, row_stride, block_size, eob, off, d_out, total,
+  TRY(st.launched(launch_zerorun_emit(d_src, nblk, row_stride, block_size, eob, scratch, off, d_out, total,
                                       st.ctx->stream), "zerorun_encode"));
   TRY(st.out(out, d_out, (size_t)total * 4));
   return st.sync();

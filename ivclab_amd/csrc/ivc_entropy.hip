@@ -267,15 +267,25 @@ struct ZwMask {
   int cnt;
 };
 
+// OR over the 16 lanes of a DPP row (quad_perm 1,0,3,2; 2,3,0,1; row_half_mirror;
+// row_mirror): VALU only, no LDS round trips
+__device__ __forceinline__ uint32_t or_row16(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false);
+  v |= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false);
+  return v;
+}
+
 __device__ __forceinline__ ZwMask zw_mask(zv4 x, int lane) {
   const uint32_t nib = (uint32_t)(x.x != 0) | (uint32_t)(x.y != 0) << 1 |
                        (uint32_t)(x.z != 0) << 2 | (uint32_t)(x.w != 0) << 3;
-  unsigned long long m = (unsigned long long)nib << (4 * (lane & 15));
-#pragma unroll
-  for (int d = 1; d < 16; d <<= 1) m |= __shfl_xor(m, d);
+  const int i = lane & 15;
+  const uint32_t lo = or_row16(i < 8 ? nib << (4 * i) : 0u);
+  const uint32_t hi = or_row16(i >= 8 ? nib << (4 * (i - 8)) : 0u);
   ZwMask z;
-  z.m = m;
-  const int last = m ? 63 - __builtin_clzll(m) : -1;
+  z.m = (uint64_t)hi << 32 | lo;
+  const int last = z.m ? 63 - __builtin_clzll(z.m) : -1;
   const uint64_t inside = last < 0 ? 0ull : (last == 63 ? ~0ull : ((1ull << (last + 1)) - 1));
   const uint64_t zeros = ~z.m & inside;
   z.st = zeros & ~(zeros << 1);
@@ -283,59 +293,109 @@ __device__ __forceinline__ ZwMask zw_mask(zv4 x, int lane) {
   return z;
 }
 
+// Unconditional 16-byte load (past-the-end blocks read the last block and are dropped by
+// the caller): no exec-masked loads, so the compiler's vmcnt waits stay exact.
 __device__ __forceinline__ zv4 zw_load(const int32_t* src, int64_t nblk, int64_t b0, int u,
                                         int lane) {
-  const int64_t blk = b0 + 4 * u + (lane >> 4);
-  if (blk >= nblk) return zv4{0, 0, 0, 0};
+  int64_t blk = b0 + 4 * u + (lane >> 4);
+  blk = blk < nblk ? blk : nblk - 1;
   return __builtin_nontemporal_load(reinterpret_cast<const zv4*>(src + blk * 64) + (lane & 15));
 }
 
+// The wide path scans per-ZW_BLK-block group counts (nblk / 16 int32 written and scanned,
+// not nblk); the emit pass derives each block's offset from its group's offset and the
+// counts of the group's earlier blocks, and writes offsets[blk] itself.
 #ifndef IVC_ZW_COUNT_GROUPS
 #define IVC_ZW_COUNT_GROUPS 4   // 16-block groups per wave-iteration of the count pass (4: -2%)
 #endif
 __global__ __launch_bounds__(256) void zw_count_kernel(const int32_t* __restrict__ src, int64_t nblk,
-                                                       int32_t* __restrict__ counts) {
+                                                       int32_t* __restrict__ gcounts) {
   constexpr int NGR = IVC_ZW_COUNT_GROUPS;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
   for (int64_t b0 = wave * ZW_BLK * NGR; b0 < nblk; b0 += nw * ZW_BLK * NGR) {
     zv4 x[NGR * ZW_LOADS];
 #pragma unroll
     for (int u = 0; u < NGR * ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
 #pragma unroll
-    for (int u = 0; u < NGR * ZW_LOADS; ++u) {
-      const ZwMask z = zw_mask(x[u], lane);
-      const int64_t blk = b0 + 4 * u + (lane >> 4);
-      if ((lane & 15) == 0 && blk < nblk) counts[blk] = z.cnt;
+    for (int g = 0; g < NGR; ++g) {
+      int tot = 0;
+#pragma unroll
+      for (int l = 0; l < ZW_LOADS; ++l) {
+        const int u = g * ZW_LOADS + l;
+        const ZwMask z = zw_mask(x[u], lane);
+        const int c = b0 + 4 * u + (lane >> 4) < nblk ? z.cnt : 0;
+        // lanes 0, 16, 32, 48 hold the load's four blocks
+        tot += __builtin_amdgcn_readlane(c, 0) + __builtin_amdgcn_readlane(c, 16) +
+               __builtin_amdgcn_readlane(c, 32) + __builtin_amdgcn_readlane(c, 48);
+      }
+      const int64_t gi = b0 / ZW_BLK + g;
+      if (lane == 0 && gi < ng) gcounts[gi] = tot;
     }
   }
 }
 
+#ifndef IVC_ZW_EMIT_GROUPS
+#define IVC_ZW_EMIT_GROUPS 4   // 16-block groups loaded per wave-iteration of the emit pass (1: +11%, 8: +11%)
+#endif
+#ifndef IVC_ZW_BRANCHFREE
+#define IVC_ZW_BRANCHFREE 1
+#endif
+constexpr int ZW_STAGE_D = ZW_STAGE + (IVC_ZW_BRANCHFREE ? 64 : 0);   // + lanes' dummy words
 __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict__ src, int64_t nblk,
-                                                      int32_t eob, const int64_t* __restrict__ off,
+                                                      int32_t eob, const int64_t* __restrict__ goff,
+                                                      int64_t* __restrict__ off,
                                                       int32_t* __restrict__ out, int64_t capacity) {
-  __shared__ int32_t stage[4 * ZW_STAGE];
+  __shared__ int32_t stage[4 * ZW_STAGE_D];
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  int32_t* zs = stage + (threadIdx.x >> 6) * ZW_STAGE;
-  const int i = lane & 15;
+  int32_t* zs = stage + (threadIdx.x >> 6) * ZW_STAGE_D;
+  const int i = lane & 15, q = lane >> 4;
   const uint64_t low = i == 0 ? 0ull : (~0ull >> (64 - 4 * i));   // positions below 4i
-  for (int64_t b0 = wave * ZW_BLK; b0 < nblk; b0 += nw * ZW_BLK) {
-    zv4 x[ZW_LOADS];
+  constexpr int EG = IVC_ZW_EMIT_GROUPS;
+  for (int64_t b00 = wave * ZW_BLK * EG; b00 < nblk; b00 += nw * ZW_BLK * EG) {
+    zv4 xx[EG * ZW_LOADS];
 #pragma unroll
-    for (int u = 0; u < ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
-    const int64_t bend = b0 + ZW_BLK < nblk ? b0 + ZW_BLK : nblk;
-    const int64_t wbase = off[b0], wend = off[bend];
+    for (int u = 0; u < EG * ZW_LOADS; ++u) xx[u] = zw_load(src, nblk, b00, u, lane);
+#pragma unroll
+   for (int gg = 0; gg < EG; ++gg) {
+    const int64_t b0 = b00 + gg * ZW_BLK;
+    if (b0 >= nblk) break;                                        // wave-uniform
+    const zv4* x = xx + gg * ZW_LOADS;
+    const int64_t g = b0 / ZW_BLK;
+    const int64_t wbase = goff[g], wend = goff[g + 1];
+    int run = 0;                                                  // symbols of earlier blocks
 #pragma unroll
     for (int u = 0; u < ZW_LOADS; ++u) {
       const ZwMask z = zw_mask(x[u], lane);
-      const int64_t blk = b0 + 4 * u + (lane >> 4);
-      if (blk < nblk) {
-        int p = (int)(off[blk] - wbase) + __builtin_popcountll(z.m & low) +
-                2 * __builtin_popcountll(z.st & low);
+      const int64_t blk = b0 + 4 * u + q;
+      const bool live = blk < nblk;
+      const int c = live ? z.cnt : 0;
+      const int c0 = __builtin_amdgcn_readlane(c, 0), c1 = __builtin_amdgcn_readlane(c, 16),
+                c2 = __builtin_amdgcn_readlane(c, 32), c3 = __builtin_amdgcn_readlane(c, 48);
+      const int bpre = run + (q > 0 ? c0 : 0) + (q > 1 ? c1 : 0) + (q > 2 ? c2 : 0);
+      run += c0 + c1 + c2 + c3;
+      if (live) {
+        if (i == 0) off[blk] = wbase + bpre;   // the block offsets: 4 x 8 B per load
+        int p = bpre + __builtin_popcountll(z.m & low) + 2 * __builtin_popcountll(z.st & low);
         const int32_t v[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+#if IVC_ZW_BRANCHFREE
+        // two ds_write per coefficient, no exec branches: a value (or a run's 0) at p, a
+        // run's length at p + 1; lanes with nothing to write hit their private dummy word
+        const uint32_t mb = (uint32_t)(z.m >> (4 * i)) & 15u, sb = (uint32_t)(z.st >> (4 * i)) & 15u;
+        int32_t* dummy = zs + ZW_STAGE + lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool nz = (mb >> j) & 1u, rs = (sb >> j) & 1u;
+          const int run = __builtin_ctzll(z.m >> (4 * i + j));
+          *(nz || rs ? zs + p : dummy) = v[j];              // v[j] == 0 at a run start
+          *(rs ? zs + p + 1 : dummy) = run;
+          p += (int)nz + 2 * (int)rs;
+        }
+#else
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int pos = 4 * i + j;
@@ -348,7 +408,8 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
             p += 2;
           }
         }
-        if (i == 0) zs[(int)(off[blk] - wbase) + z.cnt - 1] = eob;
+#endif
+        if (i == 0) zs[bpre + z.cnt - 1] = eob;
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -359,6 +420,7 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
     for (int k = lane; k < n; k += 64)
       if (k < lim) out[wbase + k] = zs[k];
     __builtin_amdgcn_wave_barrier();
+   }
   }
 }
 
@@ -373,16 +435,63 @@ static unsigned zw_grid(int64_t nblk, int per_cu) {
   return (unsigned)(grid < 1 ? 1 : grid);
 }
 
-// off[0..nblk]: exclusive symbol offsets of the blocks, off[nblk] = stream length.
-// Scratch: counts int32[nblk], agg int64[scan_scratch_elems(nblk)].
+// group offsets goff[0..ng] and the stream length at off[nblk]
+struct GroupOffsetSink {
+  int64_t* goff;
+  int64_t ng;
+  int64_t* total;
+  __device__ void operator()(int64_t i, int64_t excl, int64_t v) const {
+    goff[i] = excl;
+    if (i == ng - 1) {
+      goff[ng] = excl + v;
+      *total = excl + v;
+    }
+  }
+};
+
+// Scratch of launch_zerorun_offsets / launch_zerorun_emit: per-block int32 counts (generic
+// path) or per-group int32 counts + int64 group offsets (wide path), and the scan's
+// aggregates.
+int64_t zerorun_scratch_bytes(int64_t nblk) {
+  const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
+  const int64_t wide = ((4 * ng + 7) & ~int64_t(7)) + 8 * (ng + 1);
+  const int64_t cnt = 4 * nblk > wide ? 4 * nblk : wide;
+  return ((cnt + 7) & ~int64_t(7)) + 8 * scan_scratch_elems(nblk);
+}
+
+namespace {
+struct ZrScratch {
+  int32_t* counts;   // per block (generic) or per group (wide)
+  int64_t* goff;     // wide path: ng + 1 group offsets
+  int64_t* agg;
+};
+ZrScratch zr_scratch(void* scratch, int64_t nblk) {
+  const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
+  const int64_t wide = ((4 * ng + 7) & ~int64_t(7)) + 8 * (ng + 1);
+  const int64_t cnt = 4 * nblk > wide ? 4 * nblk : wide;
+  char* b = (char*)scratch;
+  ZrScratch z;
+  z.counts = (int32_t*)b;
+  z.goff = (int64_t*)(b + ((4 * ng + 7) & ~int64_t(7)));
+  z.agg = (int64_t*)(b + ((cnt + 7) & ~int64_t(7)));
+  return z;
+}
+}  // namespace
+
+// off[nblk] = stream length (always); the generic path also writes off[0..nblk) here, the
+// wide path in launch_zerorun_emit.
 hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, int B,
-                                  int32_t* counts, int64_t* agg, int64_t* off, hipStream_t s) {
+                                  void* scratch, int64_t* off, hipStream_t s) {
   if (nblk <= 0) return hipMemsetAsync(off, 0, sizeof(int64_t), s);
-  if (zw_ok(src, stride, B))
-    zw_count_kernel<<<zw_grid((nblk + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(src, nblk, counts);
-  else
-    zr_count_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, counts);
-  return device_scan<int64_t>(nblk, CountGen{counts}, SumI64{}, OffsetSink{off, nblk}, agg, s);
+  const ZrScratch z = zr_scratch(scratch, nblk);
+  if (zw_ok(src, stride, B)) {
+    const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
+    zw_count_kernel<<<zw_grid((nblk + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(src, nblk, z.counts);
+    return device_scan<int64_t>(ng, CountGen{z.counts}, SumI64{}, GroupOffsetSink{z.goff, ng, off + nblk},
+                                z.agg, s);
+  }
+  zr_count_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, z.counts);
+  return device_scan<int64_t>(nblk, CountGen{z.counts}, SumI64{}, OffsetSink{off, nblk}, z.agg, s);
 }
 
 // off[0..n] = exclusive int64 prefix of counts[0..n), off[n] = total (agg: scratch of
@@ -393,14 +502,18 @@ hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* 
   return device_scan<int64_t>(n, CountGen{counts}, SumI64{}, OffsetSink{off, n}, agg, s);
 }
 
-// symbols of every block at its offset; symbols at or past `capacity` are not written
+// symbols of every block at its offset; symbols at or past `capacity` are not written.
+// `scratch` is launch_zerorun_offsets' (same src/nblk).
 hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
-                               const int64_t* off, int32_t* out, int64_t capacity, hipStream_t s) {
+                               void* scratch, int64_t* off, int32_t* out, int64_t capacity,
+                               hipStream_t s) {
   if (nblk <= 0) return hipSuccess;
-  if (zw_ok(src, stride, B))
-    zw_emit_kernel<<<zw_grid(nblk, 6), 256, 0, s>>>(src, nblk, eob, off, out, capacity);
-  else
+  if (zw_ok(src, stride, B)) {
+    const ZrScratch z = zr_scratch(scratch, nblk);
+    zw_emit_kernel<<<zw_grid((nblk + IVC_ZW_EMIT_GROUPS - 1) / IVC_ZW_EMIT_GROUPS, 6), 256, 0, s>>>(src, nblk, eob, z.goff, off, out, capacity);
+  } else {
     zr_emit_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, eob, off, out, capacity);
+  }
   return hipGetLastError();
 }
 

@@ -56,10 +56,12 @@ hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* 
 hipError_t launch_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                                 int C, const QTab& t, int32_t eob, int32_t* out, int64_t capacity,
                                 int64_t* nsym, hipStream_t s);
+int64_t zerorun_scratch_bytes(int64_t nblk);
 hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, int B,
-                                  int32_t* counts, int64_t* agg, int64_t* off, hipStream_t s);
+                                  void* scratch, int64_t* off, hipStream_t s);
 hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
-                               const int64_t* off, int32_t* out, int64_t capacity, hipStream_t s);
+                               void* scratch, int64_t* off, int32_t* out, int64_t capacity,
+                               hipStream_t s);
 int64_t zr_decode_scratch_bytes(int64_t n);
 hipError_t launch_rgb2ycbcr(const void* src, int dtype, int64_t npix, double* dst, hipStream_t s);
 hipError_t launch_ycbcr2rgb(const void* src, int dtype, int64_t npix, int64_t cstride, void* dst,

@@ -806,10 +806,17 @@ __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b,
     uint32_t byte = 0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) byte |= (uint32_t)(val[p][k] != 0) << k;
-    uint64_t lm = live ? (uint64_t)byte << (8 * r) : 0ull;
-    lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 1);
-    lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 2);
-    lm |= (uint64_t)__shfl_xor((unsigned long long)lm, 4);
+    // OR over the block's 8 lanes by DPP (quad_perm 1,0,3,2; 2,3,0,1; row_half_mirror):
+    // VALU only, no LDS round trips
+    uint32_t lo = live && r < 4 ? byte << (8 * r) : 0u;
+    uint32_t hi = live && r >= 4 ? byte << (8 * (r - 4)) : 0u;
+    lo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0xB1, 0xf, 0xf, false);
+    hi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0xB1, 0xf, 0xf, false);
+    lo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0x4E, 0xf, 0xf, false);
+    hi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0x4E, 0xf, 0xf, false);
+    lo |= (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0x141, 0xf, 0xf, false);
+    hi |= (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0x141, 0xf, 0xf, false);
+    const uint64_t lm = (uint64_t)hi << 32 | lo;
     const int last = lm ? 63 - __builtin_clzll(lm) : -1;
     const uint64_t inside = last < 0 ? 0ull : (last == 63 ? ~0ull : ((1ull << (last + 1)) - 1));
     const uint64_t zeros = ~lm & inside;
@@ -821,9 +828,9 @@ __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b,
   const int c2 = cnt[NP - 1];
   const int tb = cnt[0] + cnt[1] + c2;                       // the block's symbols
   if constexpr (OUTM == OUT_COUNT) {
-    int v = r == 0 ? tb : 0;
+    int v = 0;                                                // lane 8b holds block b's total
 #pragma unroll
-    for (int d = 8; d < 64; d <<= 1) v += __shfl_xor(v, d);
+    for (int bb = 0; bb < 8; ++bb) v += __builtin_amdgcn_readlane(tb, 8 * bb);
     if (lane == 0) a.zr_counts[gid] = v;
   } else {
     // exclusive prefix of the block totals over b (lane groups of 8)

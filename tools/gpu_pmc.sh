@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT="$GRAFT_REPO_ROOT/gpurun_out/pmc"
 mkdir -p "$OUT"
-CMD=${CMD:-"python bench.py --steps 3 --warmup 1 --no-inter --no-cpu"}
+CMD=${CMD:-"python bench.py --steps 3 --warmup 1 --no-inter --no-cpu --no-pmc"}
 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 i=0
 while read -r grp; do

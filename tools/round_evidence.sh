@@ -17,12 +17,12 @@ if [ -z "$SKIP_TESTS" ]; then
 fi
 timeout -k 10 900 python bench.py ${BENCH_ARGS} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
 cat gpurun_out/bench_$TAG.json
-timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python bench.py --no-cpu ${BENCH_ARGS} > gpurun_out/prof_$TAG.log 2>&1 || { tail -20 gpurun_out/prof_$TAG.log; exit 1; }
-python tools/prof_summary.py gpurun_out/prof_$TAG gpurun_out/${TAG}_bench_kernels.md "rocprofv3 --kernel-trace --stats -- python bench.py --no-cpu ${BENCH_ARGS}" || true
+timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_$TAG" -o run -- python bench.py --no-cpu --no-pmc ${BENCH_ARGS} > gpurun_out/prof_$TAG.log 2>&1 || { tail -20 gpurun_out/prof_$TAG.log; exit 1; }
+python tools/prof_summary.py gpurun_out/prof_$TAG gpurun_out/${TAG}_bench_kernels.md "rocprofv3 --kernel-trace --stats -- python bench.py --no-cpu --no-pmc ${BENCH_ARGS}" || true
 find gpurun_out/prof_$TAG -name "*kernel_trace.csv" -delete
 head -8 gpurun_out/${TAG}_bench_kernels.md
 if [ -z "$SKIP_PMC" ]; then
-  PMC_GROUPS=tools/pmc_groups_hbm.txt CMD="python bench.py --steps 3 --warmup 1 --no-inter --no-cpu" \
+  PMC_GROUPS=tools/pmc_groups_hbm.txt CMD="python bench.py --steps 3 --warmup 1 --no-inter --no-cpu --no-pmc" \
     timeout -k 10 900 bash tools/gpu_pmc.sh > gpurun_out/pmc_$TAG.log 2>&1 || { tail -20 gpurun_out/pmc_$TAG.log; exit 1; }
   python tools/pmc_traffic.py gpurun_out/pmc/summary.json 256 2160 3840 gpurun_out/pmc_intra_latest.json
 fi
