@@ -340,19 +340,22 @@ __global__ __launch_bounds__(256) void zw_count_kernel(const int32_t* __restrict
 #ifndef IVC_ZW_EMIT_GROUPS
 #define IVC_ZW_EMIT_GROUPS 4   // 16-block groups loaded per wave-iteration of the emit pass (1: +11%, 8: +11%)
 #endif
-#ifndef IVC_ZW_BRANCHFREE
-#define IVC_ZW_BRANCHFREE 1
+#ifndef IVC_ZW_STORE4
+#define IVC_ZW_STORE4 1
 #endif
-constexpr int ZW_STAGE_D = ZW_STAGE + (IVC_ZW_BRANCHFREE ? 64 : 0);   // + lanes' dummy words
+// per wave: the symbols of a group staged at word (address of out[wbase] / 4 mod 4, so LDS
+// and stream share 16-byte alignment), then each lane's dummy word
+constexpr int ZW_STAGE_D = ZW_STAGE + 4 + 64;
 __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict__ src, int64_t nblk,
                                                       int32_t eob, const int64_t* __restrict__ goff,
                                                       int64_t* __restrict__ off,
                                                       int32_t* __restrict__ out, int64_t capacity) {
-  __shared__ int32_t stage[4 * ZW_STAGE_D];
+  __shared__ __attribute__((aligned(16))) int32_t stage[4 * ZW_STAGE_D];
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  int32_t* zs = stage + (threadIdx.x >> 6) * ZW_STAGE_D;
+  int32_t* const zbase = stage + (threadIdx.x >> 6) * ZW_STAGE_D;
+  int32_t* const dummy = zbase + ZW_STAGE + 4 + (threadIdx.x & 63);
   const int i = lane & 15, q = lane >> 4;
   const uint64_t low = i == 0 ? 0ull : (~0ull >> (64 - 4 * i));   // positions below 4i
   constexpr int EG = IVC_ZW_EMIT_GROUPS;
@@ -367,6 +370,9 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
     const zv4* x = xx + gg * ZW_LOADS;
     const int64_t g = b0 / ZW_BLK;
     const int64_t wbase = goff[g], wend = goff[g + 1];
+    // (the caller's stream need not start 16-byte aligned: the shift follows the address)
+    const int sh = IVC_ZW_STORE4 ? (int)(((uintptr_t)(out + wbase) >> 2) & 3u) : 0;
+    int32_t* const zs = zbase + sh;
     int run = 0;                                                  // symbols of earlier blocks
 #pragma unroll
     for (int u = 0; u < ZW_LOADS; ++u) {
@@ -382,11 +388,9 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
         if (i == 0) off[blk] = wbase + bpre;   // the block offsets: 4 x 8 B per load
         int p = bpre + __builtin_popcountll(z.m & low) + 2 * __builtin_popcountll(z.st & low);
         const int32_t v[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
-#if IVC_ZW_BRANCHFREE
         // two ds_write per coefficient, no exec branches: a value (or a run's 0) at p, a
         // run's length at p + 1; lanes with nothing to write hit their private dummy word
         const uint32_t mb = (uint32_t)(z.m >> (4 * i)) & 15u, sb = (uint32_t)(z.st >> (4 * i)) & 15u;
-        int32_t* dummy = zs + ZW_STAGE + lane;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const bool nz = (mb >> j) & 1u, rs = (sb >> j) & 1u;
@@ -395,20 +399,6 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
           *(rs ? zs + p + 1 : dummy) = run;
           p += (int)nz + 2 * (int)rs;
         }
-#else
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int pos = 4 * i + j;
-          if ((z.m >> pos) & 1ull) {
-            zs[p] = v[j];
-            p += 1;
-          } else if ((z.st >> pos) & 1ull) {
-            zs[p] = 0;
-            zs[p + 1] = __builtin_ctzll(z.m >> pos);   // run ends before the last nonzero
-            p += 2;
-          }
-        }
-#endif
         if (i == 0) zs[bpre + z.cnt - 1] = eob;
       }
     }
@@ -416,9 +406,27 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
     // the ZW_BLK blocks' symbols are the contiguous range [wbase, wend); written while they
     // fit the caller's capacity
     const int n = (int)(wend - wbase);
+#if IVC_ZW_STORE4
+    // 16-byte stores of the aligned quads (LDS words 4t .. 4t + 3 = stream words wbase - sh +
+    // 4t ..); the partial quads at the ends and past capacity go word by word
+    const int64_t A = wbase - sh;
+    const int nq = (sh + n + 3) >> 2;
+    for (int t = lane; t < nq; t += 64) {
+      const int w0 = 4 * t;
+      const int64_t ga = A + w0;
+      if (w0 >= sh && w0 + 4 <= sh + n && ga + 4 <= capacity) {
+        *reinterpret_cast<zv4*>(out + ga) = *reinterpret_cast<const zv4*>(zbase + w0);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (w0 + e >= sh && w0 + e < sh + n && ga + e < capacity) out[ga + e] = zbase[w0 + e];
+      }
+    }
+#else
     const int64_t lim = capacity - wbase;
     for (int k = lane; k < n; k += 64)
       if (k < lim) out[wbase + k] = zs[k];
+#endif
     __builtin_amdgcn_wave_barrier();
    }
   }

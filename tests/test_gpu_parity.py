@@ -715,6 +715,34 @@ def test_zerorun_device_wide_and_general(nblk):
     assert torch.equal(off2, off) and np.array_equal(out2.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_zerorun_device_unaligned_stream(shift):
+    """The wide path's 16-byte stream stores when the caller's output starts 4, 8 or 12 bytes
+    past a 16-byte boundary (a view into a larger buffer), with a capacity that cuts a quad."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    nblk = 1024 * 16 + 5
+    rng = np.random.default_rng(100 + shift)
+    x = rng.integers(-40, 41, (nblk, 64)).astype(np.int32)
+    x[rng.random((nblk, 64)) > rng.random((nblk, 1))] = 0
+    want = O.zerorun_encode_fast(x)
+    blocks = torch.from_numpy(x).cuda()
+    off = torch.empty(nblk + 1, dtype=torch.int64, device="cuda")
+    buf = torch.full((want.size + 8,), -1, dtype=torch.int32, device="cuda")
+    D.zerorun_encode(blocks, off, buf[shift:shift + want.size])
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    assert (got[:shift] == -1).all() and (got[shift + want.size:] == -1).all()
+    assert np.array_equal(got[shift:shift + want.size], want)
+    cap = want.size // 2 + 1
+    buf.fill_(-1)
+    D.zerorun_encode(blocks, off, buf[shift:shift + cap])
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    assert int(off[-1]) == want.size
+    assert np.array_equal(got[shift:shift + cap], want[:cap]) and (got[shift + cap:] == -1).all()
+
+
 def test_zerorun_after_fused_intra():
     """The codec chain: fused intra encode with zig-zag -> zero-run stream -> decode ->
     back to the quantised blocks, against the oracle's chain."""
