@@ -227,7 +227,8 @@ __global__ __launch_bounds__(256) void zr_emit_kernel(const int32_t* __restrict_
       const int64_t cnt = __builtin_popcountll(z.m) + 2 * __builtin_popcountll(z.starts) + 1;
       // the stream is written only while it fits the caller's capacity
       const int64_t lim = capacity - base;
-      const bool nz = (z.m >> lane) & 1ull, st = (z.starts >> lane) & 1ull;
+      const bool nz = __builtin_amdgcn_inverse_ballot_w64(z.m),      // lane bits of the masks
+                 st = __builtin_amdgcn_inverse_ballot_w64(z.starts);
       const int64_t p = (int64_t)popc_below(z.m) + 2 * (int64_t)popc_below(z.starts);
       if (nz && p < lim) out[base + p] = x[u];
       if (st) {

@@ -739,6 +739,8 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
   int32_t* zs = os;
   int64_t base = gbase;
   int fill = 0;
+  // (16-byte stores of aligned quads, as in zw_emit_kernel, measured slower here: 10.96 vs
+  // 10.38 ms — a group's ~107 symbols are two dword stores per lane)
   auto flush = [&]() {
     __builtin_amdgcn_wave_barrier();
     const int64_t lim = a.zr_cap - base;
@@ -762,20 +764,29 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
       const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
       const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
                       2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
-      const bool nz = (m >> lane) & 1ull, rs = (st >> lane) & 1ull;
+      // this lane's bits of m and st: the ballot's own predicate, and st as a lane mask
+      // (one v_cndmask on the SGPR pair instead of a 64-bit shift-and-test)
+      const bool nz = x != 0;
+      const bool rs = __builtin_amdgcn_inverse_ballot_w64(st);
       // slot pos: a nonzero, a run's 0, or — on lane last + 1, whose pos is cnt - 1 — the EOB;
       // slot pos + 1: a run's length (it ends before the last nonzero), or the EOB after a
       // nonzero lane 63.  Inactive lanes write a private dummy word (no exec branches).
       const bool w1 = nz || rs || lane == last + 1;
-      const bool w2 = rs || (lane == 63 && last == 63);
-      const int32_t v1 = nz ? x : (rs ? 0 : a.zr_eob);
+      const int32_t v1 = nz || rs ? x : a.zr_eob;           // x == 0 at a run start
       const int32_t v2 = rs ? __builtin_ctzll(m >> lane) : a.zr_eob;
       constexpr int R1 = (C == 1 && DUP) ? 2 : 1;   // plane 2 repeats plane 1's symbols
       const int reps = p == 1 ? R1 : 1;
       for (int k = 0; k < reps; ++k) {
-        if (fill + cnt > ZR_WIN - 64) flush();
-        zs[w1 ? fill + pos : ZR_WIN - 64 + lane] = v1;
-        zs[w2 ? fill + pos + 1 : ZR_WIN - 64 + lane] = v2;
+        if (fill + cnt > ZR_WIN - 65) flush();
+        // one address per lane: slot pos + 1 is written first (a run's length, the EOB after
+        // a nonzero lane 63 — both have w1 — or a don't-care that the next write fixes: after
+        // a lane's single symbol comes the next emitting lane's first slot, or the next
+        // block-plane's, which is written later or lies past `fill`), then slot pos;
+        // lanes with nothing to write hit their dummy words
+        int32_t* const d = w1 ? zs + fill + pos : zs + ZR_WIN - 65 + lane;
+        d[1] = v2;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // keep the two writes ordered
+        d[0] = v1;
         fill += cnt;
       }
     }

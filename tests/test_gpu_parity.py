@@ -857,6 +857,34 @@ def test_intra_symbols_device_and_4k():
     assert np.array_equal(short.cpu().numpy(), want[:12345])
 
 
+@pytest.mark.parametrize("shift", [1, 2, 3])
+def test_intra_symbols_unaligned_stream(shift):
+    """The fused emit's 16-byte stores when the output view starts 4/8/12 bytes past a 16-byte
+    boundary, whole and capacity-cut in the middle of a quad."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(shift)
+    img = rng.integers(0, 256, (1, 272, 480), dtype=np.uint8)
+    img[0, :64, :128] = 77
+    table = PatchQuant(0.5).get_quantization_table()
+    want = _zr_chain(img[..., None], table.astype(np.float64))
+    fr = torch.from_numpy(img).cuda()
+    nsym = torch.zeros(1, dtype=torch.int64, device="cuda")
+    buf = torch.full((want.size + 8,), -1, dtype=torch.int32, device="cuda")
+    D.intra_symbols(fr, table, buf[shift:shift + want.size], nsym)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    assert int(nsym.item()) == want.size
+    assert np.array_equal(got[shift:shift + want.size], want)
+    assert (got[:shift] == -1).all() and (got[shift + want.size:] == -1).all()
+    cap = want.size // 2 + 1
+    buf.fill_(-1)
+    D.intra_symbols(fr, table, buf[shift:shift + cap], nsym)
+    torch.cuda.synchronize()
+    got = buf.cpu().numpy()
+    assert np.array_equal(got[shift:shift + cap], want[:cap]) and (got[shift + cap:] == -1).all()
+
+
 # ------------------------------------------------------------------------- colour ------
 def test_color_golden_gpu(golden):
     from ivclab_amd.signal.color import rgb2gray, rgb2ycbcr, ycbcr2rgb
