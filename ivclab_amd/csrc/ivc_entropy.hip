@@ -345,8 +345,8 @@ __global__ __launch_bounds__(256) void zw_count_kernel(const int32_t* __restrict
 #define IVC_ZW_STORE4 1
 #endif
 // per wave: the symbols of a group staged at word (address of out[wbase] / 4 mod 4, so LDS
-// and stream share 16-byte alignment), then each lane's dummy word
-constexpr int ZW_STAGE_D = ZW_STAGE + 4 + 64;
+// and stream share 16-byte alignment), then each lane's dummy words (2, overlapping)
+constexpr int ZW_STAGE_D = ZW_STAGE + 4 + 68;   // dummy words: 64 lanes + 1, padded to 16 B
 __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict__ src, int64_t nblk,
                                                       int32_t eob, const int64_t* __restrict__ goff,
                                                       int64_t* __restrict__ off,
@@ -389,17 +389,24 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
         if (i == 0) off[blk] = wbase + bpre;   // the block offsets: 4 x 8 B per load
         int p = bpre + __builtin_popcountll(z.m & low) + 2 * __builtin_popcountll(z.st & low);
         const int32_t v[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
-        // two ds_write per coefficient, no exec branches: a value (or a run's 0) at p, a
-        // run's length at p + 1; lanes with nothing to write hit their private dummy word
+        // two ds_write per coefficient at one address, no exec branches: first every slot
+        // p + 1 (a run's length, or a don't-care), then every slot p (a value or a run's 0):
+        // the slot after a single symbol is the first slot of the next symbol, written in the
+        // second round (or the block's EOB, written after); lanes with nothing to write hit
+        // their dummy words
         const uint32_t mb = (uint32_t)(z.m >> (4 * i)) & 15u, sb = (uint32_t)(z.st >> (4 * i)) & 15u;
+        int32_t* d[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const bool nz = (mb >> j) & 1u, rs = (sb >> j) & 1u;
-          const int run = __builtin_ctzll(z.m >> (4 * i + j));
-          *(nz || rs ? zs + p : dummy) = v[j];              // v[j] == 0 at a run start
-          *(rs ? zs + p + 1 : dummy) = run;
+          d[j] = nz || rs ? zs + p : dummy;
           p += (int)nz + 2 * (int)rs;
         }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j][1] = __builtin_ctzll(z.m >> (4 * i + j));   // run length
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the rounds stay ordered
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j][0] = v[j];                // v[j] == 0 at a run start
         if (i == 0) zs[bpre + z.cnt - 1] = eob;
       }
     }
