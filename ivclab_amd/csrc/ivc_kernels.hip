@@ -757,8 +757,11 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
     for (int p = 0; p < NP; ++p) {
       const int32_t x = xv[b][p];
       const uint64_t m = __ballot(x != 0);
-      const int last = m ? 63 - __builtin_clzll(m) : -1;
-      const uint64_t inside = last < 0 ? 0ull : (last == 63 ? ~0ull : ((1ull << (last + 1)) - 1));
+      // scalar mask algebra kept short (the CU's one scalar unit issues about as many
+      // instructions per group as each SIMD's VALU): last + 1 = 64 - clz, inside = bits [0, last]
+      const int lz = m ? __builtin_clzll(m) : 64;
+      const int last1 = 64 - lz;                                  // last + 1 (0: no nonzero)
+      const uint64_t inside = m ? ~0ull >> lz : 0ull;
       const uint64_t zeros = ~m & inside;
       const uint64_t st = zeros & ~(zeros << 1);
       const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
@@ -771,7 +774,7 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
       // slot pos: a nonzero, a run's 0, or — on lane last + 1, whose pos is cnt - 1 — the EOB;
       // slot pos + 1: a run's length (it ends before the last nonzero), or the EOB after a
       // nonzero lane 63.  Inactive lanes write a private dummy word (no exec branches).
-      const bool w1 = nz || rs || lane == last + 1;
+      const bool w1 = nz || rs || lane == last1;
       const int32_t v1 = nz || rs ? x : a.zr_eob;           // x == 0 at a run start
       const int32_t v2 = rs ? __builtin_ctzll(m >> lane) : a.zr_eob;
       constexpr int R1 = (C == 1 && DUP) ? 2 : 1;   // plane 2 repeats plane 1's symbols
