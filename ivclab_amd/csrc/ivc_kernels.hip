@@ -750,9 +750,13 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
     base += fill;
     fill = 0;
   };
+  constexpr int R1 = (C == 1 && DUP) ? 2 : 1;     // plane 2 repeats plane 1's symbols
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
     if (b >= nb) break;                         // wave-uniform
+    int cnt[NP], pos[NP];
+    bool w1[NP];
+    int32_t v1[NP], v2[NP];
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int32_t x = xv[b][p];
@@ -764,9 +768,9 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
       const uint64_t inside = m ? ~0ull >> lz : 0ull;
       const uint64_t zeros = ~m & inside;
       const uint64_t st = zeros & ~(zeros << 1);
-      const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
-      const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
-                      2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
+      cnt[p] = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
+      pos[p] = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
+               2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
       // this lane's bits of m and st: the ballot's own predicate, and st as a lane mask
       // (one v_cndmask on the SGPR pair instead of a 64-bit shift-and-test)
       const bool nz = x != 0;
@@ -774,23 +778,29 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
       // slot pos: a nonzero, a run's 0, or — on lane last + 1, whose pos is cnt - 1 — the EOB;
       // slot pos + 1: a run's length (it ends before the last nonzero), or the EOB after a
       // nonzero lane 63.  Inactive lanes write a private dummy word (no exec branches).
-      const bool w1 = nz || rs || lane == last1;
-      const int32_t v1 = nz || rs ? x : a.zr_eob;           // x == 0 at a run start
-      const int32_t v2 = rs ? __builtin_ctzll(m >> lane) : a.zr_eob;
-      constexpr int R1 = (C == 1 && DUP) ? 2 : 1;   // plane 2 repeats plane 1's symbols
-      const int reps = p == 1 ? R1 : 1;
-      for (int k = 0; k < reps; ++k) {
-        if (fill + cnt > ZR_WIN - 65) flush();
+      w1[p] = nz || rs || lane == last1;
+      v1[p] = nz || rs ? x : a.zr_eob;                      // x == 0 at a run start
+      v2[p] = rs ? __builtin_ctzll(m >> lane) : a.zr_eob;
+    }
+    // one window check per block (its <= 3 x 97 symbols always fit an empty window)
+    int tb = 0;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) tb += (p == 1 ? R1 : 1) * cnt[p];
+    if (fill + tb > ZR_WIN - 65) flush();
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int k = 0; k < (p == 1 ? R1 : 1); ++k) {
         // one address per lane: slot pos + 1 is written first (a run's length, the EOB after
         // a nonzero lane 63 — both have w1 — or a don't-care that the next write fixes: after
         // a lane's single symbol comes the next emitting lane's first slot, or the next
         // block-plane's, which is written later or lies past `fill`), then slot pos;
         // lanes with nothing to write hit their dummy words
-        int32_t* const d = w1 ? zs + fill + pos : zs + ZR_WIN - 65 + lane;
-        d[1] = v2;
+        int32_t* const d = w1[p] ? zs + fill + pos[p] : zs + ZR_WIN - 65 + lane;
+        d[1] = v2[p];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // keep the two writes ordered
-        d[0] = v1;
-        fill += cnt;
+        d[0] = v1[p];
+        fill += cnt[p];
       }
     }
   }
