@@ -1546,6 +1546,9 @@ hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t
 // the rest go to per-workgroup LDS bins; one global add per bin per workgroup at the end.
 // ======================================================================================
 constexpr int HIST_HOT_LO = -3, HIST_HOT_N = 8, HIST_UNROLL = 4;
+#ifndef IVC_HIST_PACKED
+#define IVC_HIST_PACKED 1
+#endif
 
 template <typename S>
 __device__ __forceinline__ int hist_bin(S v, int64_t lo, int32_t nbins) {
@@ -1569,23 +1572,44 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
   uint32_t hot[HIST_HOT_N];
 #pragma unroll
   for (int k = 0; k < HIST_HOT_N; ++k) hot[k] = 0;
+#if IVC_HIST_PACKED
+  // the hot counts of the current iteration as 8 byte lanes of one 64-bit register (one
+  // shift and one add per symbol instead of 8 compare-adds), unpacked into `hot` after every
+  // iteration (<= 16 symbols per thread, far below a byte's 255)
+  uint64_t pk = 0;
+  auto unpack = [&]() {
+#pragma unroll
+    for (int k = 0; k < HIST_HOT_N; ++k) hot[k] += (uint32_t)(pk >> (8 * k)) & 0xffu;
+    pk = 0;
+  };
+#endif
   auto count = [&](S v) {
     // unsigned difference: v - HIST_HOT_LO wraps instead of overflowing for v near INT64_MAX
     const uint64_t u = (uint64_t)(int64_t)v - (uint64_t)(int64_t)HIST_HOT_LO;
+#if IVC_HIST_PACKED
+    const bool h = u < (uint64_t)HIST_HOT_N;
+    pk += h ? 1ull << (8u * ((uint32_t)u & 7u)) : 0ull;
+    if (!h) {
+#else
     if (u < (uint64_t)HIST_HOT_N) {
 #pragma unroll
       for (int k = 0; k < HIST_HOT_N; ++k) hot[k] += u == (uint64_t)k ? 1u : 0u;
     } else {
+#endif
       const int b = hist_bin(v, lo, nbins);
       if (use_lds) atomicAdd(&bins[b], 1u);
       else atomicAdd(&hist[b], 1ull);
     }
   };
+#if !IVC_HIST_PACKED
+  auto unpack = [&]() {};
+#endif
   // a stream that does not start on 16 B: the first `head` symbols apart
   constexpr int PER = 16 / (int)sizeof(S);
   int64_t head = (int64_t)(((16u - ((uintptr_t)sym & 15u)) & 15u) / sizeof(S));
   if (head > n) head = n;
   if (blockIdx.x == 0 && tid < head) count(sym[tid]);
+  unpack();
   sym += head;
   n -= head;
   // 16 B per lane, HIST_UNROLL loads in flight per iteration (the stream is read once)
@@ -1601,13 +1625,16 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
     for (int u = 0; u < HIST_UNROLL; ++u)
 #pragma unroll
       for (int k = 0; k < PER; ++k) count(x[u][k]);
+    unpack();
   }
   for (; i < nv; i += stride) {
     const vec_t a = __builtin_nontemporal_load(sv + i);
 #pragma unroll
     for (int k = 0; k < PER; ++k) count(a[k]);
+    unpack();
   }
   if (blockIdx.x == 0 && tid < (int)(n - nv * PER)) count(sym[nv * PER + tid]);
+  unpack();
   // hot counters: wave sums, added by lane 0 to the (clamped) bin of each hot value
 #pragma unroll
   for (int k = 0; k < HIST_HOT_N; ++k) {
