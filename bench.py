@@ -226,6 +226,18 @@ def lib_sha256():
         return hashlib.sha256(fh.read()).hexdigest()
 
 
+def csrc_sha256():
+    """Hash of the HIP sources libivc is built from (stable across rebuilds of the same code):
+    the key of the committed PMC traffic record that multi-rank runs report."""
+    d = os.path.join(ROOT, "ivclab_amd", "csrc")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        if f.endswith((".hip", ".h")):
+            with open(os.path.join(d, f), "rb") as fh:
+                h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
 # ---------------------------------------------------------------- HBM traffic (PMC) -----
 INTRA_KERNEL_MATCH = "fused_encode_kernel<unsigned char, double, double, 1,"
 
@@ -440,7 +452,8 @@ def leg_intra(args, dist, rank, world, dev, table, result, verify):
         with open(pmc) as fh:
             rec = json.load(fh)
         if (rec.get("frames") == F and rec.get("H") == H and rec.get("W") == W
-                and rec.get("libivc_sha256") == lib_sha256()):
+                and (rec.get("libivc_sha256") == lib_sha256()
+                     or rec.get("csrc_sha256") == csrc_sha256())):
             traffic = rec.get("hbm_bytes_per_launch")
             tsrc = rec.get("source")
     result.update({
