@@ -188,3 +188,22 @@ def test_huffman_host_coder():
     assert bits == L[m + 1000].sum()
     H = -(p * np.log2(p)).sum()
     assert H <= (p * L).sum() < H + 1
+
+
+def test_pmc_record_key_matches_bench():
+    """The committed HBM-traffic record (profiles/pmc_intra_latest.json) is keyed by the HIP
+    source hash that bench.py computes; tools/pmc_traffic.py writes the same key."""
+    import importlib.util
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    mods = {}
+    for name, path in (("bench", "bench.py"), ("pmc_traffic", "tools/pmc_traffic.py")):
+        spec = importlib.util.spec_from_file_location("_t_" + name, os.path.join(root, path))
+        m = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(m)
+        mods[name] = m
+    key = mods["bench"].csrc_sha256()
+    assert key == mods["pmc_traffic"].csrc_sha256() and len(key) == 64
+    rec = json.load(open(os.path.join(root, "profiles", "pmc_intra_latest.json")))
+    assert {"hbm_bytes_per_launch", "frames", "H", "W", "csrc_sha256"} <= set(rec)
+    assert 0.99 < rec["hbm_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
