@@ -12,6 +12,9 @@ libivc.so build, or null), `cpu_baseline` times the reference's algorithm (oracl
 
 Also reported from the same run (each with its own timing; none of them is `value`):
   zerorun / image2symbols  ZeroRunCoder on the zig-zag output, and pixels -> symbols fused
+  decode                   IntraCodec.symbols2image of that stream on the device (zero-run
+                           decode -> dequantise -> IDCT -> unpatch -> ycbcr2rgb), HBM roofline
+                           of the coefficient-to-image kernel
   exchange                 global Huffman-table input: alphabet bounds (all-reduce) and the
                            symbol histogram (all-gather), as IntraCodec trains it
   inter                    configs[3]: 1080p x 300, +-16 full-search ME + MC + residual
@@ -60,6 +63,7 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 DOT4_PEAK_T = 256 * 4 * 64 * 2.4e9 / 4 / 1e12
 F64_PEAK_T = 78.6 / 2
 HIST_LO, HIST_BINS = -4096, 8192
+PACE_MARGIN = 0.02             # settle the store pace this far below its lowest failed rate
 METRIC = "Mpixels/s: 4K intra DCT+quant and ±16 full-search ME, 1/2/4/8 MI355X"
 
 
@@ -424,10 +428,31 @@ def leg_intra(args, dist, rank, world, dev, table, result, verify):
         D.intra_encode(frames, table, out, zigzag=args.zigzag)
 
     L = N.lib()
-    wall, kern_ms = timed(dist, step, args.steps, args.warmup, sync_warmup=True,
-                          on_start=lambda: N.check(L.ivc_store_pace_reset_stats()))
+    # Store-pace calibration (untimed, before the W warm-up steps): the rate the paced store
+    # sweep sustains differs from box to box, and the K timed launches are
+    # enqueued without synchronisation, so they all run at the rate set before them.  Each
+    # calibration launch is synchronised so the controller folds its measurement before the
+    # next; after the warm-up the rate is settled to the last rate that held its schedule,
+    # PACE_MARGIN below the lowest rate that fell off it.
+    for _ in range(args.pace_calibrate):
+        step()
+        torch.cuda.synchronize()
+    pre = {}
+
+    def on_start():
+        N.check(L.ivc_store_pace_settle(PACE_MARGIN))
+        pre["trace"] = N.pace_trace()
+        pre["settled_GBs"] = round(L.ivc_store_pace(), 1)
+        N.check(L.ivc_store_pace_reset_stats())
+
+    wall, kern_ms = timed(dist, step, args.steps, args.warmup, sync_warmup=True, on_start=on_start)
     # the timed launches' pacing measurements (late-slot fraction, event-timed GB/s)
     pace = N.pace_stats() or {"rate_GBs": round(L.ivc_store_pace(), 1)}
+    pace["settled_GBs"] = pre["settled_GBs"]
+    pace["trace_fields"] = ["rate_GBs", "late_fraction", "achieved_GBs", "start_lag_us",
+                            "first_late_slot_frac", "next_rate_GBs", "late_fraction_startup"]
+    pace["trace_calibration_and_warmup"] = pre["trace"]
+    pace["trace_timed"] = N.pace_trace()
     # write-stream ceiling for this buffer: the same 12 B/px of int32 output written by
     # torch's vectorised fill kernel (no reads) — what the store side alone can reach
     _, fill_ms = timed(None, lambda: out.fill_(0), 3, 1)
@@ -552,6 +577,49 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
         "entropy_bits_per_symbol": round(entropy_bits(pmf), 4), "ms": round(exchange_ms, 3),
         "collective": f"all_reduce + all_gather_into_tensor ({coll_name(dist)})"
         if dist is not None else "none (1 rank)"}
+    return sym
+
+
+def leg_decode(args, dist, rank, world, dev, table, out, sym, result, verify):
+    """IntraCodec.symbols2image of the cfg3 stream (intracodec.py:84-146 with a 3-D shape:
+    zero-run decode -> un-zig-zag -> dequantise -> IDCT -> unpatch -> ycbcr2rgb), and the
+    coefficient-to-image kernel alone with its HBM roofline (36 B/px: 3 x 4 B int32 in,
+    3 x 8 B float64 out)."""
+    import ivclab_amd.device as D
+    F, h, w = out.shape[:3]
+    H, W = 8 * h, 8 * w
+    img = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
+    err = torch.zeros(3, dtype=torch.int64, device=dev)
+    cwall, cms = timed(dist, lambda: D.intra_decode_image(out, table, img, unzigzag=True, to_rgb=True),
+                       3, 1)
+    swall, sms = timed(dist, lambda: D.symbols2image(sym, 3, table, img, err, to_rgb=True), 3, 1)
+    px = F * H * W
+    algo = px * 36
+    result["decode"] = {
+        "metric": "Mpixels/s: IntraCodec.symbols2image of the cfg3 stream (3-plane YCbCr -> RGB float64)",
+        "value": round(world * px / sms / 1e3, 1), "unit": "Mpixels/s", "ms": round(sms, 3),
+        "symbols_per_gpu": int(sym.numel()),
+        "roofline": {"bound": "hbm", "kernel": "intra_decode_kernel<C=3,zz,image,rgb>",
+                     "kernel_ms": round(cms, 4), "achieved": round(algo / (cms * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(algo / (cms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "algorithmic_bytes_per_launch": algo,
+                     "note": "coefficients [F,h,w,3,64] int32 -> unpatched RGB [F,H,W,3] float64: "
+                             "12 B in + 24 B out per pixel"},
+        "zerorun_decode_ms": round(sms - cms, 3),
+    }
+    if verify is not None:
+        torch.cuda.synchronize()
+        from oracle import ivc_oracle as O
+        if err.tolist() != [0, 0, 0]:
+            verify["failures"].append(f"decode: stream verdict {err.tolist()}")
+        for f in sorted({0, F - 1}):
+            want = O.ycbcr2rgb(O.unpatch(O.intra_decode(out[f].cpu().numpy(), 1.0, unzigzag=True)))
+            check_equal(img[f].cpu().numpy(), want, f"decode frame {f}", verify["failures"])
+        verify["checked"].append(f"decode: symbols2image frames [0, {F - 1}] whole vs oracle "
+                                 "(unflatten, dequantise, IDCT, unpatch, ycbcr2rgb)")
+    del img
+    torch.cuda.empty_cache()
 
 
 def leg_inter(args, dist, rank, world, dev, table, result, verify):
@@ -813,10 +881,14 @@ def parse(argv=None):
                     help="frames of the float64 ME leg (a prefix of the cfg4 sequence)")
     ap.add_argument("--sr", type=int, default=16)
     ap.add_argument("--zigzag", action="store_true")
+    ap.add_argument("--pace-calibrate", type=int, default=12,
+                    help="synchronised untimed launches of the headline kernel before the warm-up "
+                         "that let the store-pace controller find this box's rate")
     ap.add_argument("--no-inter", action="store_true")
     ap.add_argument("--no-intra", action="store_true", help="profiling aid: skip the cfg3 leg")
     ap.add_argument("--no-symbols", action="store_true", help="skip the zero-run/exchange legs")
     ap.add_argument("--no-f64", action="store_true", help="skip the float64 ME leg")
+    ap.add_argument("--no-decode", action="store_true", help="skip the symbols2image leg")
     ap.add_argument("--no-class-api", action="store_true", help="skip the host-buffer leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-sharded", action="store_true", help="skip the cfg5 8K leg")
@@ -865,7 +937,10 @@ def main():
         args.frames = 1
     frames, out = leg_intra(args, dist, rank, world, dev, table, result, verify)
     if not args.no_symbols:
-        leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify)
+        sym = leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify)
+        if not args.no_decode:
+            leg_decode(args, dist, rank, world, dev, table, out, sym, result, verify)
+        del sym
     del out, frames
     torch.cuda.empty_cache()
 

@@ -74,10 +74,25 @@ double ivc_store_pace_late(void);
  * (encoder 0 = image source, 1 = inter residual), folding every completed launch first:
  * out[0] launches measured, [1] launches over the late threshold, [2] mean and [3] maximum
  * late fraction, [4] current rate (GB/s), [5] last late fraction, [6] mean achieved GB/s of
- * the measured launches (bytes / event time), [7] measurements still in flight.  Writes
- * min(n, 8) values and returns that count (a negative status on a bad argument).          */
+ * the measured launches (bytes / event time), [7] measurements still in flight, [8] launches
+ * over the late threshold that still moved at least their schedule's rate, [9] the lowest
+ * rate that fell off its schedule (0: none yet).  Writes min(n, 10) values and returns that
+ * count (a negative status on a bad argument).                                             */
 int ivc_store_pace_stats(int encoder, double* out, int n);
 int ivc_store_pace_reset_stats(void);
+/* Per-launch trace since the last reset: the most recent min(max_records, available, 256)
+ * measured launches, oldest first, 7 doubles each: rate the launch ran at (GB/s), late-slot
+ * fraction past each wave's start-up slots (its first min(64, slots / 8); what the rate adapts
+ * on), achieved GB/s (bytes / event time), the kernel's first workgroup entry minus the
+ * schedule origin (us), the earliest late slot past the start-up as a fraction of a wave's
+ * slots (-1: none), the rate after folding it, the late fraction of the start-up slots.
+ * Returns the number of records written.  (ivc_store_pace_stats' late fractions are those
+ * past the start-up.)                                                                      */
+int ivc_store_pace_trace(int encoder, double* out, int max_records);
+/* Drop the current device's rates to the last rate that held its schedule and to at most
+ * (1 - margin) x the lowest rate that fell off it: for callers about to enqueue many launches
+ * without synchronisation (they all run at one rate).                                      */
+int ivc_store_pace_settle(double margin);
 
 /* ---------------------------------------------------------------- DCT -------------- */
 /* 2-D DCT-II (inverse=0) / DCT-III (inverse=1) of nblk contiguous 8x8 blocks, applied along
@@ -142,6 +157,29 @@ int ivc_intra_decode(const int32_t* q, int64_t nblk, const double* table, int ca
                      int unzigzag, double* out);
 int ivc_intra_decode_dev(const int32_t* q, int64_t nblk, const double* table, int calc_dtype,
                          int unzigzag, double* out, void* stream);
+
+/* The decode chain with the unpatch fused: q [nframes][H/8][W/8][C][64] int32 (C = 1 or 3;
+ * zig-zag order when unzigzag) -> out [nframes][H][W][3] float64 =
+ * rearrange(DCT.inverse_transform(PatchQuant.dequantize(ZigZag.unflatten(q))),
+ *           'hp wp c h w -> (hp h) (wp w) c')
+ * (C = 1 broadcasts over the 3 table planes, patchquant.py:77); to_rgb = 1 applies ycbcr2rgb
+ * (color.py:40-63) to the result.
+ * Replaces IntraCodec.symbols2image after the zero-run decode  intracodec.py:115-141       */
+int ivc_intra_decode_image(const int32_t* q, int64_t nframes, int64_t H, int64_t W, int C,
+                           const double* table, int unzigzag, int to_rgb, double* out);
+int ivc_intra_decode_image_dev(const int32_t* q, int64_t nframes, int64_t H, int64_t W, int C,
+                               const double* table, int unzigzag, int to_rgb, double* out,
+                               void* stream);
+/* IntraCodec.symbols2image (intracodec.py:84-146) for 8x8 blocks of 64 coefficients: the
+ * zero-run decode of nsym symbols into nframes x H/8 x W/8 x C blocks (errors reported in
+ * err[3] exactly as ivc_zerorun_decode; out is then undefined), then ivc_intra_decode_image
+ * with unzigzag = 1, all on the device.  The caller crops and squeezes as the reference does. */
+int ivc_symbols2image(const int32_t* sym, int64_t nsym, int64_t nframes, int64_t H, int64_t W,
+                      int C, const double* table, int32_t eob, int to_rgb, double* out,
+                      int64_t* err);
+int ivc_symbols2image_dev(const int32_t* sym, int64_t nsym, int64_t nframes, int64_t H, int64_t W,
+                          int C, const double* table, int32_t eob, int to_rgb, double* out,
+                          int64_t* err, void* stream);
 
 /* ---------------------------------------------------------------- motion ----------- */
 /* Full-search block matching, 8x8 blocks, displacement +-sr, SSD, first strict minimum in

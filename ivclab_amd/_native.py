@@ -46,6 +46,8 @@ _SIGS = {
     "ivc_store_pace_late": ([], _ct.c_double),
     "ivc_store_pace_stats": ([_I, _P, _I], _I),
     "ivc_store_pace_reset_stats": ([], _I),
+    "ivc_store_pace_trace": ([_I, _P, _I], _I),
+    "ivc_store_pace_settle": ([_ct.c_double], _I),
     "ivc_set_histogram_occupancy": ([_I], _I),
     "ivc_histogram_occupancy": ([], _I),
     "ivc_dct8x8": ([_P, _I, _L, _P, _I, _I, _I], _I),
@@ -61,6 +63,10 @@ _SIGS = {
                               _ct.c_int32, _P], _I),
     "ivc_intra_decode": ([_P, _L, _P, _I, _I, _P], _I),
     "ivc_intra_decode_dev": ([_P, _L, _P, _I, _I, _P, _P], _I),
+    "ivc_intra_decode_image": ([_P, _L, _L, _L, _I, _P, _I, _I, _P], _I),
+    "ivc_intra_decode_image_dev": ([_P, _L, _L, _L, _I, _P, _I, _I, _P, _P], _I),
+    "ivc_symbols2image": ([_P, _L, _L, _L, _L, _I, _P, _ct.c_int32, _I, _P, _P], _I),
+    "ivc_symbols2image_dev": ([_P, _L, _L, _L, _L, _I, _P, _ct.c_int32, _I, _P, _P, _P], _I),
     "ivc_motion_estimate": ([_P, _P, _I, _L, _L, _L, _I, _I, _P], _I),
     "ivc_motion_estimate_dev": ([_P, _P, _I, _L, _L, _L, _I, _I, _P, _P], _I),
     "ivc_motion_compensate": ([_P, _I, _L, _L, _L, _L, _P, _I, _P], _I),
@@ -171,15 +177,26 @@ def ptr(a: np.ndarray) -> int:
 def pace_stats(encoder: int = 0):
     """Store-pacing measurements of the current device since the last reset
     (ivc_store_pace_stats), as a dict; None when no launch was measured."""
-    out = np.zeros(8, np.float64)
-    n = lib().ivc_store_pace_stats(encoder, out.ctypes.data, 8)
+    out = np.zeros(10, np.float64)
+    n = lib().ivc_store_pace_stats(encoder, out.ctypes.data, 10)
     check(min(n, 0), "pace_stats")
     if out[0] < 1:
         return None
     return {"launches_measured": int(out[0]), "launches_over_late_threshold": int(out[1]),
             "late_fraction_mean": round(float(out[2]), 4), "late_fraction_max": round(float(out[3]), 4),
             "rate_GBs": round(float(out[4]), 1), "late_fraction_last": round(float(out[5]), 4),
-            "achieved_GBs_mean": round(float(out[6]), 1)}
+            "achieved_GBs_mean": round(float(out[6]), 1),
+            "late_but_on_pace": int(out[8]), "lowest_failed_rate_GBs": round(float(out[9]), 1)}
+
+
+def pace_trace(encoder: int = 0, max_records: int = 256):
+    """Per-launch store-pacing trace since the last reset (ivc_store_pace_trace), oldest
+    first: [rate GB/s, late fraction past the start-up, achieved GB/s, start lag us, first late
+    slot past the start-up, next rate, late fraction of the start-up slots]."""
+    out = np.zeros((max_records, 7), np.float64)
+    n = lib().ivc_store_pace_trace(encoder, out.ctypes.data, max_records)
+    check(min(n, 0), "pace_trace")
+    return [[round(float(v), 4 if i in (1, 4, 6) else 1) for i, v in enumerate(r)] for r in out[:n]]
 
 
 def table_arg(table: np.ndarray) -> np.ndarray:

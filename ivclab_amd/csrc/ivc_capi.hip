@@ -216,6 +216,20 @@ int ivc_store_pace_reset_stats(void) {
   return IVC_OK;
 }
 
+int ivc_store_pace_trace(int encoder, double* out, int max_records) {
+  if (encoder < 0 || encoder > 1 || max_records < 0 || (max_records > 0 && !out))
+    return fail(IVC_E_ARG, "ivc_store_pace_trace: encoder must be 0 or 1, out must hold "
+                           "7 * max_records values");
+  return store_pace_trace(encoder, out, max_records);
+}
+
+int ivc_store_pace_settle(double margin) {
+  if (!(margin >= 0 && margin < 0.5))
+    return fail(IVC_E_ARG, "ivc_store_pace_settle: margin must be in [0, 0.5)");
+  store_pace_settle(margin);
+  return IVC_OK;
+}
+
 int ivc_set_histogram_occupancy(int wg_per_cu) {
   if (wg_per_cu < 0 || wg_per_cu > 16)
     return fail(IVC_E_ARG, "ivc_set_histogram_occupancy: wg_per_cu must be in [0, 16]");
@@ -391,7 +405,7 @@ int ivc_intra_decode_dev(const int32_t* q, int64_t nblk, const double* table, in
                          int unzigzag, double* out, void* stream) {
   CHECK(nblk >= 0, IVC_E_SHAPE, "intra_decode: negative block count");
   CHECK(calc_dtype == IVC_F64, IVC_E_DTYPE, "intra_decode: int32 symbols dequantise in float64");
-  CHECK(aligned16(out), IVC_E_ARG, "intra_decode_dev: output must be 16-byte aligned");
+  CHECK(aligned16(q) && aligned16(out), IVC_E_ARG, "intra_decode_dev: pointers must be 16-byte aligned");
   QTab t;
   TRY(load_table(table, &t));
   return dev_launch(launch_intra_decode(q, nblk, t, unzigzag, out, (hipStream_t)stream),
@@ -414,6 +428,113 @@ int ivc_intra_decode(const int32_t* q, int64_t nblk, const double* table, int ca
   TRY(st.launched(launch_intra_decode((const int32_t*)d_in, nblk, t, unzigzag, d_out,
                                       st.ctx->stream), "intra_decode"));
   TRY(st.out(out, d_out, ob));
+  return st.sync();
+}
+
+static int check_zr_dec(int64_t nsym, int64_t nblk, int32_t B) {
+  CHECK(nsym >= 0 && nsym < (1LL << 32), IVC_E_ARG, "zerorun_decode: need 0 <= nsym < 2^32");
+  CHECK(nblk >= 0, IVC_E_ARG, "zerorun_decode: nblk must be >= 0");
+  CHECK(B >= 0 && B <= 64, IVC_E_SHAPE, "zerorun_decode: block_size must be in [0, 64]");
+  return IVC_OK;
+}
+
+static int check_decode_image(int64_t nframes, int64_t H, int64_t W, int C, const char* what) {
+  TRY(check_frames(nframes, H, W, what));
+  CHECK(C == 1 || C == 3, IVC_E_SHAPE, std::string(what) + ": C must be 1 or 3 (the dequantiser "
+                                       "broadcasts the channel axis against 3 table planes)");
+  return IVC_OK;
+}
+
+int ivc_intra_decode_image_dev(const int32_t* q, int64_t nframes, int64_t H, int64_t W, int C,
+                               const double* table, int unzigzag, int to_rgb, double* out,
+                               void* stream) {
+  TRY(check_decode_image(nframes, H, W, C, "intra_decode_image"));
+  CHECK(aligned16(q) && aligned16(out), IVC_E_ARG, "intra_decode_image_dev: pointers must be 16-byte aligned");
+  QTab t;
+  TRY(load_table(table, &t));
+  return dev_launch(launch_intra_decode_image(q, nframes, H, W, C, t, unzigzag, to_rgb, out,
+                                              (hipStream_t)stream), "intra_decode_image");
+}
+
+int ivc_intra_decode_image(const int32_t* q, int64_t nframes, int64_t H, int64_t W, int C,
+                           const double* table, int unzigzag, int to_rgb, double* out) {
+  TRY(check_decode_image(nframes, H, W, C, "intra_decode_image"));
+  QTab t;
+  TRY(load_table(table, &t));
+  const int64_t npx = nframes * H * W;
+  if (npx == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t ib = (size_t)npx / 64 * C * 64 * 4, ob = (size_t)npx * 3 * 8;
+  void* d_in = st.in(q, ib);
+  double* d_out = (double*)st.alloc(ob);
+  if (st.status) return st.status;
+  TRY(st.launched(launch_intra_decode_image((const int32_t*)d_in, nframes, H, W, C, t, unzigzag,
+                                            to_rgb, d_out, st.ctx->stream), "intra_decode_image"));
+  TRY(st.out(out, d_out, ob));
+  return st.sync();
+}
+
+// symbols -> zero-run decode (zerorun.py:46-88, errors as results in err[3]) -> the image
+// decode above, on the device without host hops
+static int symbols2image_enqueue(const int32_t* sym, int64_t nsym, int64_t nframes, int64_t H,
+                                 int64_t W, int C, const QTab& t, int32_t eob, int to_rgb,
+                                 double* out, int64_t* err, void* coef, void* scratch,
+                                 hipStream_t s) {
+  const int64_t nblk = nframes * (H / 8) * (W / 8) * C;
+  TRY(dev_launch(launch_zerorun_decode(sym, nsym, nblk, 64, eob, (int32_t*)coef, scratch, err, s),
+                 "symbols2image: zerorun_decode"));
+  return dev_launch(launch_intra_decode_image((const int32_t*)coef, nframes, H, W, C, t, 1, to_rgb,
+                                              out, s), "symbols2image: intra_decode_image");
+}
+
+int ivc_symbols2image_dev(const int32_t* sym, int64_t nsym, int64_t nframes, int64_t H, int64_t W,
+                          int C, const double* table, int32_t eob, int to_rgb, double* out,
+                          int64_t* err, void* stream) {
+  TRY(check_decode_image(nframes, H, W, C, "symbols2image"));
+  TRY(check_zr_dec(nsym, nframes * (H / 8) * (W / 8) * C, 64));
+  CHECK(err, IVC_E_ARG, "symbols2image: err is NULL");
+  CHECK(aligned16(out), IVC_E_ARG, "symbols2image_dev: output must be 16-byte aligned");
+  QTab t;
+  TRY(load_table(table, &t));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t nblk = nframes * (H / 8) * (W / 8) * C;
+  void *coef = nullptr, *scratch = nullptr;
+  hipError_t e = scratch_alloc(&coef, (size_t)nblk * 256, s);
+  if (e == hipSuccess) e = scratch_alloc(&scratch, (size_t)zr_decode_scratch_bytes(nsym), s);
+  if (e != hipSuccess) {
+    if (coef) (void)hipFreeAsync(coef, s);
+    return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
+  }
+  const int rc = symbols2image_enqueue(sym, nsym, nframes, H, W, C, t, eob, to_rgb, out, err, coef,
+                                       scratch, s);
+  (void)hipFreeAsync(scratch, s);
+  (void)hipFreeAsync(coef, s);
+  return rc;
+}
+
+int ivc_symbols2image(const int32_t* sym, int64_t nsym, int64_t nframes, int64_t H, int64_t W,
+                      int C, const double* table, int32_t eob, int to_rgb, double* out,
+                      int64_t* err) {
+  TRY(check_decode_image(nframes, H, W, C, "symbols2image"));
+  const int64_t nblk = nframes * (H / 8) * (W / 8) * C;
+  TRY(check_zr_dec(nsym, nblk, 64));
+  CHECK(err, IVC_E_ARG, "symbols2image: err is NULL");
+  QTab t;
+  TRY(load_table(table, &t));
+  Staging st;
+  TRY(st.open());
+  const size_t ob = (size_t)(nframes * H * W) * 3 * 8;
+  const int32_t* d_sym = (const int32_t*)st.in(sym, (size_t)nsym * 4);
+  void* scratch = st.alloc((size_t)zr_decode_scratch_bytes(nsym));
+  void* coef = st.alloc((size_t)nblk * 256);
+  double* d_out = (double*)st.alloc(ob);
+  int64_t* d_err = (int64_t*)st.alloc(3 * 8);
+  if (st.status) return st.status;
+  TRY(symbols2image_enqueue(d_sym, nsym, nframes, H, W, C, t, eob, to_rgb, d_out, d_err, coef,
+                            scratch, st.ctx->stream));
+  TRY(st.out(out, d_out, ob));
+  TRY(st.out(err, d_err, 3 * 8));
   return st.sync();
 }
 
@@ -674,12 +795,6 @@ int ivc_zerorun_encode(const int32_t* src, int64_t nblk, int32_t row_stride, int
   return st.sync();
 }
 
-static int check_zr_dec(int64_t nsym, int64_t nblk, int32_t B) {
-  CHECK(nsym >= 0 && nsym < (1LL << 32), IVC_E_ARG, "zerorun_decode: need 0 <= nsym < 2^32");
-  CHECK(nblk >= 0, IVC_E_ARG, "zerorun_decode: nblk must be >= 0");
-  CHECK(B >= 0 && B <= 64, IVC_E_SHAPE, "zerorun_decode: block_size must be in [0, 64]");
-  return IVC_OK;
-}
 
 int ivc_zerorun_decode_dev(const int32_t* sym, int64_t nsym, int64_t nblk, int32_t block_size,
                            int32_t eob, int32_t* out, int64_t* err, void* stream) {

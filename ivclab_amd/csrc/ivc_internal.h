@@ -36,14 +36,21 @@ hipError_t launch_zigzag(const void* src, int64_t nrow, int64_t stride, int esiz
 hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                                int C, const QTab& t, int calc_dtype, int zigzag, int32_t* out,
                                hipStream_t s);
+// decode chain (ivc_decode.hip): [nblk][3][64] -> [nblk][3][8][8] f64, and
+// [F][h][w][C][64] -> [F][H][W][3] f64 image (optionally ycbcr2rgb)
 hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, int unzigzag,
                                double* out, hipStream_t s);
+hipError_t launch_intra_decode_image(const int32_t* q, int64_t nframes, int64_t H, int64_t W,
+                                     int C, const QTab& t, int unzigzag, int to_rgb, double* out,
+                                     hipStream_t s);
 // store pacing of the fused coefficient kernels (ivc_kernels.hip): target total HBM GB/s, 0 = off
 double store_pace_gbps();
 double store_pace_late_fraction();
 void set_store_pace_gbps(double gbps);
 int store_pace_stats(int kind, double* out, int n);
 void store_pace_reset_stats();
+int store_pace_trace(int kind, double* out, int max_records);
+void store_pace_settle(double margin);
 // workgroups per CU of the histogram launches (ivc_kernels.hip)
 int histogram_wg_per_cu();
 void set_histogram_wg_per_cu(int k);

@@ -13,6 +13,7 @@
 // workgroup writes its contiguous output span with 16-byte stores.  HBM traffic per unit
 // is one read of the input and one write of the output.
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <cstdlib>
 #include <mutex>
@@ -92,36 +93,22 @@ __device__ __forceinline__ void load8(const TI* __restrict__ p, TI* v) {
   }
 
 // ======================================================================================
-// Standalone 2-D DCT-II / DCT-III of contiguous 8x8 units (dct.py:12-46).  With DEQ the
-// unit is one plane of an int32 [blk][3][64] symbol block: (un-zig-zag ->) dequantise
-// (patchquant.py:77-78: int32 * table in float64, truncating cast) -> DCT-III.
+// Standalone 2-D DCT-II / DCT-III of contiguous 8x8 units (dct.py:12-46).  (The decode chain
+// dequantise -> DCT-III has its own kernel: ivc_decode.hip.)
 // ======================================================================================
-template <typename TI, typename T, bool INV, bool DEQ>
+template <typename TI, typename T, bool INV>
 __global__ __launch_bounds__(256) void dct8x8_kernel(const TI* __restrict__ src, int64_t nunit,
-                                                     T* __restrict__ dst, T fct, int ortho,
-                                                     int unzz, QTab tab) {
+                                                     T* __restrict__ dst, T fct, int ortho) {
   __shared__ __attribute__((aligned(16))) T xs[32 * 72];
   const int tid = threadIdx.x, u = tid >> 3, r = tid & 7;
   for (int64_t g = blockIdx.x; g * 32 < nunit; g += gridDim.x) {
     const int64_t unit = g * 32 + u;
     T x[8];
     if (unit < nunit) {
-      if constexpr (DEQ) {
-        const int64_t blk = unit / 3;
-        const int p = (int)(unit - blk * 3);
-        const int32_t* q = reinterpret_cast<const int32_t*>(src) + blk * 192 + p * 64;
+      alignas(16) TI v[8];
+      load8<TI>(src + unit * 64 + r * 8, v);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const int j = r * 8 + k;
-          const int32_t qv = q[unzz ? c_zz_order[j] : j];
-          x[k] = (T)np_to_i32<double>((double)qv * tab.q[p * 64 + j]);
-        }
-      } else {
-        alignas(16) TI v[8];
-        load8<TI>(src + unit * 64 + r * 8, v);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) x[k] = (T)v[k];
-      }
+      for (int k = 0; k < 8; ++k) x[k] = (T)v[k];
     } else {
 #pragma unroll
       for (int k = 0; k < 8; ++k) x[k] = T(0);
@@ -156,35 +143,25 @@ hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst
   double fct = inorm == 0 ? 1.0 : (inorm == 1 ? 0.25 : 0.0625);
   int ortho = norm == IVC_NORM_ORTHO;
   unsigned grid = grid_for(nblk, 32, 8);
-  QTab none{};
   if (dst_dtype == IVC_F32) {
     if (src_dtype != IVC_F32) return hipErrorInvalidValue;
     if (inverse)
-      dct8x8_kernel<float, float, true, false><<<grid, 256, 0, s>>>(
-          (const float*)src, nblk, (float*)dst, (float)fct, ortho, 0, none);
+      dct8x8_kernel<float, float, true><<<grid, 256, 0, s>>>((const float*)src, nblk, (float*)dst,
+                                                              (float)fct, ortho);
     else
-      dct8x8_kernel<float, float, false, false><<<grid, 256, 0, s>>>(
-          (const float*)src, nblk, (float*)dst, (float)fct, ortho, 0, none);
+      dct8x8_kernel<float, float, false><<<grid, 256, 0, s>>>((const float*)src, nblk, (float*)dst,
+                                                               (float)fct, ortho);
     return hipGetLastError();
   }
   if (dst_dtype != IVC_F64 || src_dtype == IVC_F32) return hipErrorInvalidValue;
   IVC_DISPATCH_ALL(src_dtype, {
     if (inverse)
-      dct8x8_kernel<TI, double, true, false><<<grid, 256, 0, s>>>(
-          (const TI*)src, nblk, (double*)dst, fct, ortho, 0, none);
+      dct8x8_kernel<TI, double, true><<<grid, 256, 0, s>>>((const TI*)src, nblk, (double*)dst,
+                                                           fct, ortho);
     else
-      dct8x8_kernel<TI, double, false, false><<<grid, 256, 0, s>>>(
-          (const TI*)src, nblk, (double*)dst, fct, ortho, 0, none);
+      dct8x8_kernel<TI, double, false><<<grid, 256, 0, s>>>((const TI*)src, nblk, (double*)dst,
+                                                            fct, ortho);
   });
-  return hipGetLastError();
-}
-
-hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, int unzigzag,
-                               double* out, hipStream_t s) {
-  if (nblk <= 0) return hipSuccess;
-  const int64_t nunit = nblk * 3;
-  dct8x8_kernel<int32_t, double, true, true><<<grid_for(nunit, 32, 8), 256, 0, s>>>(
-      q, nunit, out, 0.25, 1, unzigzag, t);
   return hipGetLastError();
 }
 
@@ -344,6 +321,7 @@ struct FusedArgs {
   // pace_d = 0: unpaced
   uint64_t* pace_t0;     // pace block (pace_stamp_kernel): start time, late-slot counters
   uint32_t pace_d;       // 1/256 clock ticks per slot
+  uint32_t pace_early;   // a wave's start-up slots, whose lateness is counted apart
 #ifdef IVC_ABLATION
   int ablate;            // diagnostic builds only (tools/ablate): bit mask of skipped phases
 #endif
@@ -417,12 +395,20 @@ __device__ __forceinline__ uint32_t pace_until(uint64_t t256, uint32_t slack) {
   return late;
 }
 
-// pace block: [0] start time (ticks), [1..8] late-slot counters (sharded: one atomic word
-// saturates near 90 updates/us)
-constexpr int PACE_SHARDS = 8, PACE_WORDS = 1 + PACE_SHARDS;
+// pace block: [0] schedule origin (ticks), [1..8] late-slot counters (sharded: one atomic
+// word saturates near 90 updates/us), [9] the kernel's start (earliest workgroup entry),
+// [10] the earliest late slot past the start-up window of any wave (diagnostics)
+constexpr int PACE_SHARDS = 8, PACE_START = 1 + PACE_SHARDS, PACE_FIRST_LATE = PACE_START + 1,
+              PACE_WORDS = PACE_FIRST_LATE + 1;
+// a wave's first min(PACE_EARLY, slots / 8) slots are counted apart (late counter words: early
+// slots in the low 32 bits, the rest in the high 32 bits): the start-up lateness while the grid
+// is dispatched and the first tiles arrive is not the schedule outrunning the device
+constexpr uint32_t PACE_EARLY = 64;
 __global__ void pace_stamp_kernel(uint64_t* blk, uint32_t lead) {
   blk[0] = __builtin_amdgcn_s_memrealtime() + lead;
-  for (int i = 1; i < PACE_WORDS; ++i) blk[i] = 0;
+  for (int i = 1; i < PACE_START; ++i) blk[i] = 0;
+  blk[PACE_START] = ~0ull;
+  blk[PACE_FIRST_LATE] = ~0ull;
 }
 
 
@@ -951,13 +937,27 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
 
   // pacing clock of this wave's slots (slot = groups stored so far), in 1/256 ticks
   uint64_t pace_next = 0;
-  if (OUTM == OUT_COEFS && a.pace_d)
+  if (OUTM == OUT_COEFS && a.pace_d) {
     pace_next = (*a.pace_t0 << 8) + (uint64_t)a.pace_d * (blockIdx.x * 4u + wave) / nwaves;
-  uint32_t nlate = 0;
+    if (tid == 0)
+      __hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(a.pace_t0) + PACE_START,
+                             (unsigned long long)__builtin_amdgcn_s_memrealtime(),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // late slots of the wave's first PACE_EARLY slots (start-up: the grid is still being
+  // dispatched and the first tiles loaded while the schedule runs) and of the rest
+  uint32_t nlate_early = 0, nlate = 0, pslot = 0, first_late = 0xffffffffu;
   auto store_prev = [&](uint32_t plt, int pg, bool have_prev) {
     if constexpr (OUTM == OUT_COEFS) {
       if (a.pace_d && have_prev) {
-        nlate += pace_until(pace_next, a.pace_d);
+        const uint32_t l = pace_until(pace_next, a.pace_d);
+        if (pslot < a.pace_early) {
+          nlate_early += l;
+        } else {
+          nlate += l;
+          if (l && first_late == 0xffffffffu) first_late = pslot;
+        }
+        ++pslot;
         pace_next += a.pace_d;
       }
       store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
@@ -1051,12 +1051,25 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
     }
   }
   if constexpr (OUTM == OUT_COEFS) {
-    if (a.pace_d && have_prev) nlate += pace_until(pace_next, a.pace_d);
+    if (a.pace_d && have_prev) {
+      const uint32_t l = pace_until(pace_next, a.pace_d);
+      if (pslot < a.pace_early) {
+        nlate_early += l;
+      } else {
+        nlate += l;
+        if (l && first_late == 0xffffffffu) first_late = pslot;
+      }
+    }
     store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
-    if (nlate && lane == 0)
-      __hip_atomic_fetch_add(reinterpret_cast<unsigned long long*>(a.pace_t0) + 1 +
-                                 blockIdx.x % PACE_SHARDS,
-                             (unsigned long long)nlate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((nlate | nlate_early) && lane == 0) {
+      unsigned long long* blk = reinterpret_cast<unsigned long long*>(a.pace_t0);
+      __hip_atomic_fetch_add(blk + 1 + blockIdx.x % PACE_SHARDS,
+                             (unsigned long long)nlate_early | ((unsigned long long)nlate << 32),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (nlate)
+        __hip_atomic_fetch_min(blk + PACE_FIRST_LATE, (unsigned long long)first_late,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -1111,46 +1124,70 @@ static unsigned resident_grid(K kernel, int64_t work_groups_needed) {
 
 // Store pacing of the coefficient-writing fused kernels (see pace_until).  The rate is the
 // total HBM rate (input + output bytes) the paced sweep is timed for, per device and encoder.
-// Every paced launch is measured (a ring of PACE_RING slots: the launch's late-slot counters
-// copied to pinned memory and its duration from two events), and completed measurements are
-// folded in launch order when a later launch is set up, or when the statistics are read:
-//  * late slots above PACE_LATE_HI of the launch's slots: the schedule outran the device.
-//    The rate drops to the lower of 98% of itself and 1.1x what that launch actually moved
-//    (bytes / duration; over the pace the sweep runs ~10% under it) — one measured launch
-//    brings a start rate that is far too fast back near the device's pace — and the launch's
-//    rate becomes the "too fast" mark;
-//  * otherwise the rate creeps up (+1.5% per launch while under 96% of the mark, +0.3%
-//    nearer it), never past 98% of the mark (the edge is sharp and bimodal: launches at
-//    99% of a failed rate still fail half the time), which itself rises 0.1% per good launch
-//    so a transient cannot cap the rate for good;
-//  * the first measured launch only records (it writes fresh output pages and runs slow).
-//  Fixed-rate sweeps (IVC_PACE_FIXED, two boxes): good launches hold the schedule to within
-//  ~35 us; the edge sat at 5.9 and 6.1-6.2 TB/s.
+// Every paced launch is measured: setup_pacing reserves a slot of a ring (PACE_RING) for it
+// and finish_pacing closes exactly that slot (the pace block copied to pinned memory, the
+// duration from two events), so launches from several host threads never share a slot.
+// Completed measurements are folded in launch order when a later launch is set up, or when
+// the statistics are read.  Each fold starts from the rate THAT launch ran at (S.rate): a
+// burst of launches enqueued without synchronisation all ran at one rate, and folding k of
+// their failures must not compound into 0.98^k.
+//  * late slots above PACE_LATE_HI of the launch's slots, and the launch moved less than its
+//    schedule: the schedule outran the device.  The rate drops to the lower of 98% of the
+//    launch's rate and 1.1x what it actually moved (over the pace the sweep runs ~10% under
+//    it), never below what the last good launch moved (that floor decays 2% per failure so a
+//    device that really slowed down is followed), and the launch's rate becomes the "too
+//    fast" mark;
+//  * late but the launch moved at least its schedule's rate: the lateness did not come from
+//    the rate (e.g. a schedule origin already behind when the kernel started); recorded, no
+//    step back;
+//  * otherwise the rate creeps up from the launch's rate (+1.5% per launch while under 96%
+//    of the mark, +0.3% nearer it), never past 98% of the mark (the edge is sharp and
+//    bimodal: launches at 99% of a failed rate still fail half the time), which itself rises
+//    0.1% per good launch so a transient cannot cap the rate for good;
+//  * the first measured launch of the process only records (fresh output pages: slow).
+// ivc_store_pace_settle drops the rate to the last rate that held its schedule (and below the
+// mark by a margin) — callers that enqueue many launches at once use it after a warm-up so the
+// whole burst runs at a validated rate.  Fixed-rate sweeps (IVC_PACE_FIXED, two boxes): good
+// launches hold the schedule to within ~35 us; the edge sat at 5.9 and 6.1-6.2 TB/s.
 // IVC_PACE_GBPS / ivc_set_store_pace set the starting rate (0 disables pacing).
 static std::mutex g_pace_mu;
 static double g_pace_start = -1.0;
 // late-slot fractions are bimodal: < 1% below the device's rate, 20-50% once over it
 constexpr double PACE_LATE_HI = 0.05, PACE_MAX_GBPS = 7600.0;
-constexpr int PACE_RING = 32;
+constexpr int PACE_RING = 32, PACE_TRACE = 256;
+// lead of the schedule origin over the stamp kernel's clock read (ticks of 10 ns)
+constexpr uint32_t PACE_LEAD = 300;
 
+enum PaceSlotState { PS_FREE = 0, PS_ARMED, PS_CLOSED, PS_VOID };
 struct PaceSlot {
-  uint64_t* host = nullptr;       // pinned copy of the late counters
+  uint64_t* host = nullptr;       // pinned copy of the pace block
   hipEvent_t t0 = nullptr, t1 = nullptr;  // around the kernel (timing)
-  hipEvent_t done = nullptr;      // after the counters' copy
-  double slots = 0, bytes = 0, rate = 0;
+  hipEvent_t done = nullptr;      // after the pace block's copy
+  double slots = 0, slots_per_wave = 0, bytes = 0, rate = 0;
+  int state = PS_FREE;
 };
 struct PaceStats {
-  int64_t measured = 0, over = 0;
+  int64_t measured = 0, over = 0, late_fast = 0;
   double sum_late = 0, max_late = 0, sum_gbps = 0;
+};
+// one folded measurement: rate the launch ran at, the late fraction of its slots past the
+// start-up window, event-timed GB/s, the kernel's first workgroup entry relative to the
+// schedule origin (us; > 0: origin behind), the earliest late slot past the start-up window as
+// a fraction of the slots per wave (-1: none late), the rate after the fold, the late
+// fraction of the start-up slots
+struct PaceTraceRec {
+  double rate, late, gbps, lag_us, first_late, next_rate, late_early;
 };
 struct PaceState {
   uint64_t* blk = nullptr;        // device pace block
   PaceSlot ring[PACE_RING];
-  int head = 0, count = 0;        // oldest in-flight measurement, number in flight
-  int armed = -1;                 // slot of the launch being set up
+  int head = 0, count = 0;        // oldest reserved measurement, number reserved
   double rate = 0, too_fast = 1e30, last_late = -1;
+  double good_rate = 0, good_gbps = 0;  // the last launch that held its schedule
   bool seen_first = false;        // the process's first measured launch (not adapted on)
   PaceStats st;
+  PaceTraceRec trace[PACE_TRACE];
+  int64_t ntrace = 0;             // records since the last reset (ring of PACE_TRACE)
 };
 // per device and per encoder (0: image source, 1: inter residual source)
 static PaceState g_pace[64][2];
@@ -1171,47 +1208,73 @@ static bool pace_fixed() {
   return f;
 }
 
-// Folds every completed measurement, oldest first (caller holds g_pace_mu).
-static void pace_harvest(PaceState& P) {
-  while (P.count > 0) {
-    if (P.rate <= 0) {            // pacing switched off since: drop the measurements
-      P.head = (P.head + P.count) % PACE_RING;
-      P.count = 0;
-      break;
-    }
-    PaceSlot& S = P.ring[P.head];
-    if (hipEventQuery(S.done) != hipSuccess) break;
-    uint64_t late = 0;
-    for (int i = 0; i < PACE_SHARDS; ++i) late += S.host[i];
-    float ms = 0;
-    const bool timed = hipEventElapsedTime(&ms, S.t0, S.t1) == hipSuccess && ms > 0;
-    const double f = (double)late / S.slots;
-    const double gbps = timed ? S.bytes / (ms * 1e-3) / 1e9 : 0.0;
-    P.last_late = f;
-    P.st.measured += 1;
-    P.st.sum_late += f;
-    P.st.max_late = std::max(P.st.max_late, f);
-    P.st.sum_gbps += gbps;
-    const bool first = P.st.measured == 1 && !P.seen_first;   // fresh output pages: slow
-    P.seen_first = true;
-    if (pace_fixed()) {
-      if (f > PACE_LATE_HI) P.st.over += 1;
-    } else if (first) {
-      if (f > PACE_LATE_HI) P.st.over += 1;
-    } else if (f > PACE_LATE_HI) {
-      P.st.over += 1;
+static double pace_early_slots(double slots_per_wave) {
+  return std::min<double>(PACE_EARLY, std::floor(slots_per_wave / 8));
+}
+
+// One completed measurement into the controller (caller holds g_pace_mu).
+static void pace_fold(PaceState& P, const PaceSlot& S) {
+  uint64_t late = 0, late_early = 0;
+  for (int i = 0; i < PACE_SHARDS; ++i) {
+    late_early += S.host[1 + i] & 0xffffffffull;
+    late += S.host[1 + i] >> 32;
+  }
+  float ms = 0;
+  const bool timed = hipEventElapsedTime(&ms, S.t0, S.t1) == hipSuccess && ms > 0;
+  const double early_slots = S.slots / S.slots_per_wave * pace_early_slots(S.slots_per_wave);
+  const double rest_slots = S.slots - early_slots;
+  const double f = rest_slots > 0 ? (double)late / rest_slots : 0.0;
+  const double f_early = early_slots > 0 ? (double)late_early / early_slots : 0.0;
+  const double gbps = timed ? S.bytes / (ms * 1e-3) / 1e9 : 0.0;
+  const uint64_t t0 = S.host[0], start = S.host[PACE_START], fl = S.host[PACE_FIRST_LATE];
+  const double lag_us = start != ~0ull ? ((double)(int64_t)(start - t0)) * 1e-2 : 0.0;
+  const double first_late = fl != ~0ull && S.slots_per_wave > 0 ? (double)fl / S.slots_per_wave : -1.0;
+  P.last_late = f;
+  P.st.measured += 1;
+  P.st.sum_late += f;
+  P.st.max_late = std::max(P.st.max_late, f);
+  P.st.sum_gbps += gbps;
+  const bool first = !P.seen_first;            // fresh output pages: slow
+  P.seen_first = true;
+  const bool over = f > PACE_LATE_HI;
+  if (over) P.st.over += 1;
+  if (!pace_fixed() && !first) {
+    if (over && gbps > 0 && gbps >= 0.99 * S.rate) {
+      P.st.late_fast += 1;                     // late, yet at least as fast as the schedule
+    } else if (over) {
       P.too_fast = std::min(P.too_fast, S.rate);
-      // a launch over the device's pace runs ~10% under it (late waves store out of address
-      // order), so 1.1x what it moved is about the pace; never above 98% of the failed rate
-      double r = P.rate * 0.98;
+      double r = 0.98 * S.rate;
       if (gbps > 0) r = std::min(r, 1.1 * gbps);
-      P.rate = std::max(r, 100.0);
+      r = std::max(r, P.good_gbps);
+      P.good_gbps *= 0.98;
+      P.rate = std::max(std::min(P.rate, r), 100.0);
     } else {
+      P.good_rate = S.rate;
+      P.good_gbps = gbps;
       P.too_fast *= 1.001;
       const double cap = std::min(PACE_MAX_GBPS, 0.98 * P.too_fast);
-      const double step = P.rate < 0.96 * P.too_fast ? 1.015 : 1.003;
-      P.rate = std::max(std::min(P.rate * step, cap), P.rate);
+      const double step = S.rate < 0.96 * P.too_fast ? 1.015 : 1.003;
+      P.rate = std::max(P.rate, std::min(S.rate * step, cap));
     }
+  }
+  PaceTraceRec& T = P.trace[P.ntrace % PACE_TRACE];
+  T = {S.rate, f, gbps, lag_us, first_late, P.rate, f_early};
+  P.ntrace += 1;
+}
+
+// Folds every completed measurement, oldest first (caller holds g_pace_mu).  Stops at a slot
+// whose launch is still being enqueued or whose copy has not landed.
+static void pace_harvest(PaceState& P) {
+  while (P.count > 0) {
+    PaceSlot& S = P.ring[P.head];
+    if (S.state == PS_ARMED) break;
+    if (S.state == PS_CLOSED) {
+      if (P.rate > 0) {
+        if (hipEventQuery(S.done) != hipSuccess) break;
+        pace_fold(P, S);
+      }                            // else: pacing switched off since, drop the measurement
+    }
+    S.state = PS_FREE;
     P.head = (P.head + 1) % PACE_RING;
     P.count -= 1;
   }
@@ -1249,11 +1312,28 @@ int store_pace_stats(int kind, double* out, int n) {
   if (P->blk) pace_harvest(*P);
   const PaceStats& s = P->st;
   const double m = s.measured > 0 ? (double)s.measured : 1.0;
-  const double v[8] = {(double)s.measured, (double)s.over, s.sum_late / m, s.max_late,
-                       P->blk ? P->rate : pace_start_rate(), P->last_late, s.sum_gbps / m,
-                       (double)P->count};
-  for (int i = 0; i < n && i < 8; ++i) out[i] = v[i];
-  return n < 8 ? n : 8;
+  const double v[10] = {(double)s.measured, (double)s.over, s.sum_late / m, s.max_late,
+                        P->blk ? P->rate : pace_start_rate(), P->last_late, s.sum_gbps / m,
+                        (double)P->count, (double)s.late_fast,
+                        P->too_fast < 1e29 ? P->too_fast : 0.0};
+  for (int i = 0; i < n && i < 10; ++i) out[i] = v[i];
+  return n < 10 ? n : 10;
+}
+
+int store_pace_trace(int kind, double* out, int max_records) {
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  PaceState* P = pace_state_current(kind);
+  if (!P) return 0;
+  if (P->blk) pace_harvest(*P);
+  const int64_t have = std::min<int64_t>(P->ntrace, PACE_TRACE);
+  const int64_t n = std::min<int64_t>(have, max_records);
+  for (int64_t i = 0; i < n; ++i) {         // the n most recent, oldest first
+    const PaceTraceRec& T = P->trace[(P->ntrace - n + i) % PACE_TRACE];
+    double* o = out + 7 * i;
+    o[0] = T.rate; o[1] = T.late; o[2] = T.gbps; o[3] = T.lag_us; o[4] = T.first_late;
+    o[5] = T.next_rate; o[6] = T.late_early;
+  }
+  return (int)n;
 }
 
 void store_pace_reset_stats() {
@@ -1262,7 +1342,20 @@ void store_pace_reset_stats() {
     for (auto& p : d) {
       if (p.blk) pace_harvest(p);
       p.st = PaceStats();
+      p.ntrace = 0;
     }
+}
+
+void store_pace_settle(double margin) {
+  std::lock_guard<std::mutex> g(g_pace_mu);
+  for (int kind = 0; kind < 2; ++kind) {
+    PaceState* P = pace_state_current(kind);
+    if (!P || !P->blk || P->rate <= 0) continue;
+    pace_harvest(*P);
+    if (P->good_rate > 0) P->rate = std::min(P->rate, P->good_rate);
+    if (P->too_fast < 1e29) P->rate = std::min(P->rate, (1.0 - margin) * P->too_fast);
+    P->rate = std::max(P->rate, 100.0);
+  }
 }
 
 void set_store_pace_gbps(double gbps) {
@@ -1272,6 +1365,7 @@ void set_store_pace_gbps(double gbps) {
     for (auto& p : d) {
       p.rate = g_pace_start;
       p.too_fast = 1e30;
+      p.good_rate = p.good_gbps = 0;
     }
 }
 
@@ -1281,70 +1375,78 @@ static bool pace_alloc(PaceState& P) {
     return false;
   }
   for (auto& S : P.ring) {
-    if (hipHostMalloc((void**)&S.host, 8 * PACE_SHARDS, hipHostMallocDefault) != hipSuccess ||
+    if (hipHostMalloc((void**)&S.host, 8 * PACE_WORDS, hipHostMallocDefault) != hipSuccess ||
         hipEventCreate(&S.t0) != hipSuccess || hipEventCreate(&S.t1) != hipSuccess ||
-        hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess)
-      return false;  // blk stays set: the ring is partially usable, never freed (process-long)
+        hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
+      S.host = nullptr;            // this slot (and the rest) stay unusable
+      return false;                // blk stays set: the ring is partially usable (process-long)
+    }
   }
   return true;
 }
 
 // Turns pacing on for a launch of `nwaves` persistent waves that store `slots` groups each
 // (of `group_bytes` input + output bytes): a one-lane kernel on the same stream stamps the
-// start time (the clock a few microseconds ahead, covering the launch gap) and clears the
-// late counters.  Concurrent launches on other streams may overwrite the device's pace block
-// between a stamp and its kernel; that only shifts a schedule by a launch gap or blurs one
-// launch's late count.
-static void setup_pacing(FusedArgs& a, int kind, int64_t nwaves, int64_t slots,
-                         double group_bytes, hipStream_t s) {
-  if (slots < 8) return;
+// start time (the clock PACE_LEAD ahead, covering the launch gap) and clears the counters.
+// Returns the reserved measurement slot (-1: the launch is paced but not measured), which the
+// caller hands to finish_pacing after the kernel.  Concurrent launches on other streams may
+// overwrite the device's pace block between a stamp and its kernel; that only shifts a
+// schedule by a launch gap or blurs one launch's late count.
+static int setup_pacing(FusedArgs& a, int kind, int64_t nwaves, int64_t slots,
+                        double group_bytes, hipStream_t s) {
+  if (slots < 8) return -1;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return -1;
   std::lock_guard<std::mutex> g(g_pace_mu);
   PaceState& P = g_pace[dev][kind];
-  P.armed = -1;
   if (!P.blk) {
-    if (pace_start_rate() <= 0) return;
+    if (pace_start_rate() <= 0) return -1;
     if (!pace_alloc(P)) {
       (void)hipGetLastError();
-      if (!P.blk) return;
+      if (!P.blk) return -1;
     }
     P.rate = pace_start_rate();
   }
   pace_harvest(P);
-  if (P.rate <= 0) return;
+  if (P.rate <= 0) return -1;
   // ticks (10 ns) per slot: the whole grid's slot bytes at the target rate
   const double d256 = (double)nwaves * group_bytes / (P.rate * 1e9) * 1e8 * 256.0;
-  if (!(d256 >= 1.0) || d256 > 4.0e9) return;
+  if (!(d256 >= 1.0) || d256 > 4.0e9) return -1;
+  int slot = -1;
   if (P.count < PACE_RING) {
     const int k = (P.head + P.count) % PACE_RING;
     PaceSlot& S = P.ring[k];
     if (S.host && S.done && hipEventRecord(S.t0, s) == hipSuccess) {
       S.slots = (double)nwaves * (double)slots;
+      S.slots_per_wave = (double)slots;
       S.bytes = (double)nwaves * (double)slots * group_bytes;
       S.rate = P.rate;
-      P.armed = k;
+      S.state = PS_ARMED;
+      P.count += 1;
+      slot = k;
     }
     (void)hipGetLastError();
   }
-  pace_stamp_kernel<<<1, 1, 0, s>>>(P.blk, 300u);
+  pace_stamp_kernel<<<1, 1, 0, s>>>(P.blk, PACE_LEAD);
   a.pace_t0 = P.blk;
   a.pace_d = (uint32_t)d256;
+  a.pace_early = (uint32_t)pace_early_slots((double)slots);
+  return slot;
 }
 
-// After a paced launch: close its measurement (end event, counters' copy, done event).
-static void finish_pacing(int kind, hipStream_t s) {
+// After a paced launch: close its measurement (end event, pace block copy, done event).
+static void finish_pacing(int kind, int slot, hipStream_t s) {
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
+  if (slot < 0 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return;
   std::lock_guard<std::mutex> g(g_pace_mu);
   PaceState& P = g_pace[dev][kind];
-  if (P.armed < 0) return;
-  PaceSlot& S = P.ring[P.armed];
-  P.armed = -1;
-  if (hipEventRecord(S.t1, s) == hipSuccess &&
-      hipMemcpyAsync(S.host, P.blk + 1, 8 * PACE_SHARDS, hipMemcpyDeviceToHost, s) == hipSuccess &&
-      hipEventRecord(S.done, s) == hipSuccess)
-    P.count += 1;
+  PaceSlot& S = P.ring[slot];
+  if (S.state != PS_ARMED) return;
+  const bool ok =
+      hipEventRecord(S.t1, s) == hipSuccess &&
+      hipMemcpyAsync(S.host, P.blk, 8 * PACE_WORDS, hipMemcpyDeviceToHost, s) == hipSuccess &&
+      hipEventRecord(S.done, s) == hipSuccess;
+  S.state = ok ? PS_CLOSED : PS_VOID;
   (void)hipGetLastError();
 }
 
@@ -1374,9 +1476,9 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
   auto go = [&](auto k) {
     const unsigned g = grid(k);
     const int64_t nw = 4 * (int64_t)g;
-    setup_pacing(a, SRC, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
+    const int slot = setup_pacing(a, SRC, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
     k<<<g, 256, 0, s>>>(a, t);
-    if (a.pace_d) finish_pacing(SRC, s);
+    finish_pacing(SRC, slot, s);
   };
   if (C == 1 && a.dup12) go(fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, C == 1>);
   else go(fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, false>);
@@ -1419,6 +1521,7 @@ static FusedArgs make_fused_args(const void* img, const int64_t* mv, int32_t* ou
   a.zr_eob = 0;
   a.pace_t0 = nullptr;
   a.pace_d = 0;
+  a.pace_early = 0;
   a.dup12 = 1;
   for (int i = 0; i < 64; ++i)
     if (t.q[64 + i] != t.q[128 + i]) a.dup12 = 0;
