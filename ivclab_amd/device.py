@@ -152,3 +152,36 @@ def intra_symbols(frames, table, out, nsym, eob=4000, stream=None):
     N.check(N.lib().ivc_intra_symbols_dev(frames.data_ptr(), N.DTYPE_CODE[np.dtype(np.uint8)], F, H,
                                           W, C, N.ptr(t), int(eob), out.data_ptr(), out.numel(),
                                           nsym.data_ptr(), _stream(stream)), "intra_symbols")
+
+
+def intra_decode_image(q, table, out, unzigzag=True, to_rgb=False, stream=None):
+    """q [F, h, w, C, 64] int32 (C = 1 or 3) -> out [F, 8h, 8w, 3] float64: the unpatched
+    DCT.inverse_transform(PatchQuant.dequantize(ZigZag.unflatten(q))) (C = 1 broadcasts over
+    the 3 table planes), optionally through ycbcr2rgb.  Asynchronous."""
+    import torch
+    _contig(q, "q"); _contig(out, "out")
+    if q.dtype != torch.int32 or out.dtype != torch.float64 or q.dim() != 5 or q.shape[-1] != 64:
+        raise ValueError("intra_decode_image: q [F, h, w, C, 64] int32, out float64")
+    F, h, w, C, _ = q.shape
+    if tuple(out.shape) != (F, 8 * h, 8 * w, 3):
+        raise ValueError(f"intra_decode_image: out must be {(F, 8 * h, 8 * w, 3)}")
+    t = N.table_arg(table)
+    N.check(N.lib().ivc_intra_decode_image_dev(q.data_ptr(), F, 8 * h, 8 * w, C, N.ptr(t),
+                                               int(bool(unzigzag)), int(bool(to_rgb)),
+                                               out.data_ptr(), _stream(stream)), "intra_decode_image")
+
+
+def symbols2image(sym, C, table, out, err, eob=4000, to_rgb=False, stream=None):
+    """IntraCodec.symbols2image on the device: the int32 zero-run stream of F frames of
+    [h, w, C] blocks -> out [F, 8h, 8w, 3] float64 (zero-run decode -> un-zig-zag ->
+    dequantise -> IDCT -> unpatch, optionally ycbcr2rgb).  err [3] int64 receives the
+    stream's verdict as zerorun_decode's.  Asynchronous."""
+    import torch
+    _contig(sym, "sym"); _contig(out, "out"); _contig(err, "err")
+    if sym.dtype != torch.int32 or out.dtype != torch.float64 or err.dtype != torch.int64:
+        raise ValueError("symbols2image: int32 sym, float64 out, int64 err")
+    F, H, W, _ = out.shape
+    t = N.table_arg(table)
+    N.check(N.lib().ivc_symbols2image_dev(sym.data_ptr(), sym.numel(), F, H, W, int(C), N.ptr(t),
+                                          int(eob), int(bool(to_rgb)), out.data_ptr(),
+                                          err.data_ptr(), _stream(stream)), "symbols2image")

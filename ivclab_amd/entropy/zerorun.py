@@ -73,13 +73,7 @@ class ZeroRunCoder:
         h, w, c = original_shape
         expected = h * w * c
         B = int(self.block_size)
-        is_list = not isinstance(encoded, np.ndarray)
-        sym = np.asarray(encoded)
-        if sym.ndim != 1:
-            sym = sym.reshape(-1)
-        if sym.size == 0:
-            sym = sym.astype(np.int32)
-        sym = np.ascontiguousarray(_as_int32_symbols(sym))
+        sym, is_list = decode_input(encoded)
         if expected == 0:
             # the reference rearranges an empty list: the same einops error
             return rearrange(np.array([], dtype=np.int32), "(h w c) p -> h w c p",
@@ -90,15 +84,33 @@ class ZeroRunCoder:
         err = np.zeros(3, np.int64)
         N.check(N.lib().ivc_zerorun_decode(N.ptr(sym), sym.size, expected, B, int(self.EOB),
                                            N.ptr(out), N.ptr(err)), "zerorun_decode")
-        code = int(err[0])
-        if code == 1:
-            raise ValueError(f"Block size exceeded: {int(err[1])}")
-        if code == 2:
-            raise ValueError("Unexpected end of encoded symbols")
-        if code == 3:
-            n = int(err[1])
-            raise IndexError("list index out of range" if is_list
-                             else f"index {n} is out of bounds for axis 0 with size {n}")
-        if code == 4:
-            raise ValueError(f"Expected {int(err[1])} blocks, got {int(err[2])}")
+        raise_stream_error(err, is_list)
         return out.reshape(h, w, c, B)
+
+
+def decode_input(encoded):
+    """The symbol stream as contiguous int32 (the reference reads it element by element, so
+    any 1-D sequence of integers is accepted) and whether it came as a Python list (the
+    reference's IndexError message differs between lists and arrays)."""
+    is_list = not isinstance(encoded, np.ndarray)
+    sym = np.asarray(encoded)
+    if sym.ndim != 1:
+        sym = sym.reshape(-1)
+    if sym.size == 0:
+        sym = sym.astype(np.int32)
+    return np.ascontiguousarray(_as_int32_symbols(sym)), is_list
+
+
+def raise_stream_error(err, is_list):
+    """The reference's exception for a malformed stream (err as ivc_zerorun_decode fills it)."""
+    code = int(err[0])
+    if code == 1:
+        raise ValueError(f"Block size exceeded: {int(err[1])}")
+    if code == 2:
+        raise ValueError("Unexpected end of encoded symbols")
+    if code == 3:
+        n = int(err[1])
+        raise IndexError("list index out of range" if is_list
+                         else f"index {n} is out of bounds for axis 0 with size {n}")
+    if code == 4:
+        raise ValueError(f"Expected {int(err[1])} blocks, got {int(err[2])}")

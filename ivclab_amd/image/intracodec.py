@@ -15,6 +15,7 @@ from einops import rearrange
 
 from .. import _native as N
 from ..entropy import HuffmanCoder, ZeroRunCoder, smooth_pmf, stats_marg
+from ..entropy.zerorun import decode_input, raise_stream_error
 from ..quantization import PatchQuant
 from ..signal import DiscreteCosineTransform
 from ..signal.color import rgb2ycbcr, ycbcr2rgb
@@ -75,6 +76,18 @@ class IntraCodec:
         zz_scanned = self.zigzag.flatten(quantized)
         return self.zerorun.encode(zz_scanned)
 
+    def _fused_decode(self, symbols, h, w, C, to_rgb):
+        """ivc_symbols2image: [h*8, w*8, 3] float64 (ycbcr, or RGB when to_rgb)."""
+        sym, is_list = decode_input(symbols)
+        t = N.table_arg(self.quant.get_quantization_table())
+        out = np.empty((h * 8, w * 8, 3), np.float64)
+        err = np.zeros(3, np.int64)
+        N.check(N.lib().ivc_symbols2image(N.ptr(sym), sym.size, 1, h * 8, w * 8, C, N.ptr(t),
+                                          int(self.zerorun.EOB), int(bool(to_rgb)), N.ptr(out),
+                                          N.ptr(err)), "symbols2image")
+        raise_stream_error(err, is_list)
+        return out
+
     def symbols2image(self, symbols, original_shape):
         """intracodec.py:93-146: zero-run decode -> inverse zig-zag -> dequantise -> IDCT ->
         unpatch (-> crop, ycbcr2rgb)."""
@@ -86,6 +99,13 @@ class IntraCodec:
             H, W, C = original_shape
             is_rgb = True
         patch_shape = [H // 8, W // 8, C]
+        if (tuple(self.block_shape) == (8, 8) and self.zerorun.block_size == 64 and C in (1, 3)
+                and H >= 8 and W >= 8):
+            # the whole chain on the device: zero-run decode -> un-zig-zag -> dequantise ->
+            # IDCT -> unpatch (-> ycbcr2rgb), one host call
+            # (C = 1 returns the 3 dequantised planes [h*8, w*8, 3]; a 3-D shape with C = 3
+            # ends in ycbcr2rgb; H, W not multiples of 8 decode h*8 x w*8, the crop is a no-op)
+            return self._fused_decode(symbols, H // 8, W // 8, C, to_rgb=is_rgb and C != 1)
         decoded = self.zerorun.decode(symbols, original_shape=patch_shape)
         inv_zz = self.zigzag.unflatten(decoded)
         dequant = self.quant.dequantize(inv_zz)

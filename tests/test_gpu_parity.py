@@ -413,6 +413,79 @@ def test_store_pacing_changes_timing_only():
     assert_bits(outs[5800.0][0], want, "paced 4K frame 0")
 
 
+def test_store_pace_trace_settle_and_threads():
+    """The pacing controller's per-launch trace and settle (include/ivc.h): a rate far above
+    any device's (every slot late) is stepped back from THAT launch's rate — a burst of such
+    launches folded together does not compound — and settle never raises the rate.  Two host
+    threads launching on two streams reserve distinct measurement slots: every launch is
+    measured exactly once.  Outputs stay those of the oracle throughout."""
+    torch = pytest.importorskip("torch")
+    import threading
+    import ivclab_amd.device as D
+    N, L = _native()
+    rng = np.random.default_rng(89)
+    F, H, W = 8, 2160, 3840
+    img = rng.integers(0, 256, (F, H, W, 1), dtype=np.uint8)
+    x = torch.from_numpy(img).cuda()
+    table = PatchQuant(1.0).get_quantization_table()
+    start = L.ivc_store_pace()
+    try:
+        o = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device="cuda")
+        D.intra_encode(x, table, o)                    # the process's first measured launch
+        torch.cuda.synchronize()
+        N.check(L.ivc_set_store_pace(50000.0))
+        N.check(L.ivc_store_pace_reset_stats())
+        for _ in range(4):                              # one burst, no synchronisation
+            D.intra_encode(x, table, o)
+        torch.cuda.synchronize()
+        tr = N.pace_trace()
+        assert len(tr) == 4
+        assert all(r[0] == 50000.0 for r in tr), tr     # all ran at the rate set before them
+        assert all(r[1] > 0.5 for r in tr), tr          # far too fast: most slots late
+        # no compounding: every fold steps back from 50000 once (to <= 0.98 x 50000 or 1.1x
+        # what the launch moved), never 0.98^k
+        after = L.ivc_store_pace()
+        assert 100.0 <= after <= 0.98 * 50000.0
+        assert after >= min(1.1 * r[2] for r in tr) * 0.999, (after, tr)
+        st = N.pace_stats()
+        assert st["launches_measured"] == 4 and st["launches_over_late_threshold"] == 4
+        before = L.ivc_store_pace()
+        N.check(L.ivc_store_pace_settle(0.02))
+        assert L.ivc_store_pace() <= before
+        assert L.ivc_store_pace_settle(0.7) == N.E_ARG
+        # two threads, two streams
+        N.check(L.ivc_set_store_pace(5000.0))
+        N.check(L.ivc_store_pace_reset_stats())
+        outs = [torch.empty_like(o) for _ in range(2)]
+        errs = []
+
+        def worker(i):
+            try:
+                s = torch.cuda.Stream()
+                with torch.cuda.stream(s):
+                    for _ in range(3):
+                        D.intra_encode(x, table, outs[i], stream=s)
+                s.synchronize()
+            except Exception as e:  # noqa: BLE001
+                errs.append(e)
+
+        th = [threading.Thread(target=worker, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        assert not errs, errs
+        st = N.pace_stats()
+        assert st["launches_measured"] == 6, st
+        assert all(r[2] > 0 for r in N.pace_trace()), N.pace_trace()
+    finally:
+        N.check(L.ivc_set_store_pace(start))
+    want = O.intra_encode(img[0], 1.0).reshape(H // 8, W // 8, 3, 64)
+    for oo in [o] + outs:
+        assert_bits(oo[0].cpu().numpy(), want, "paced 4K frame 0")
+
+
 def test_histogram_vs_oracle():
     N, L = _native()
     rng = np.random.default_rng(1)
@@ -963,10 +1036,72 @@ def test_intracodec_symbols_and_image(golden, case):
         ycc, rgb = img, False
     sym = codec.image2symbols(img, is_source_rgb=rgb)
     assert_bits(sym, _chain_symbols(ycc, scale), "image2symbols")
-    if case != "gray_u8_pad":
-        out_shape = img.shape
-        assert_bits(codec.symbols2image(sym, out_shape), _chain_image(sym, out_shape, scale),
-                    "symbols2image")
+    out_shape = img.shape
+    assert_bits(codec.symbols2image(sym, out_shape), _chain_image(sym, out_shape, scale),
+                "symbols2image")
+
+
+@pytest.mark.parametrize("C", [1, 3])
+@pytest.mark.parametrize("zz", [0, 1])
+@pytest.mark.parametrize("rgb", [0, 1])
+def test_intra_decode_image_vs_oracle(C, zz, rgb):
+    """ivc_intra_decode_image (the decode chain with the unpatch fused, ivc_decode.hip):
+    unflatten -> dequantise (C = 1 broadcast over 3 planes) -> IDCT -> unpatch (-> ycbcr2rgb)
+    against the oracle on 2 frames of 24 x 152 (19 block columns: ragged 8-block groups),
+    coefficients from quantised content, extremes whose dequantised value overflows int32
+    (INT32_MIN, as x86 NumPy casts) and scales down to 0.013."""
+    N, L = _native()
+    rng = np.random.default_rng(100 * C + 10 * zz + rgb)
+    F, H, W = 2, 24, 152
+    for scale in (1.0, 0.013, 2.5):
+        q = rng.integers(-60, 61, (F, H // 8, W // 8, C, 64)).astype(np.int32)
+        q[..., 0] = rng.integers(-1000, 1000, q.shape[:-1])
+        q[0, 0, 0] = np.iinfo(np.int32).max                       # dequantise overflows
+        q[1, 1, 3] = np.iinfo(np.int32).min
+        q[0, 2, 18, 0, 5] = 0
+        table = PatchQuant(scale).get_quantization_table()
+        t = N.table_arg(table)
+        out = np.full((F, H, W, 3), np.nan)
+        N.check(L.ivc_intra_decode_image(N.ptr(q), F, H, W, C, N.ptr(t), zz, rgb, N.ptr(out)))
+        for f in range(F):
+            qf = q[f] if zz else q[f].reshape(q[f].shape[:-1] + (8, 8))
+            want = O.unpatch(O.intra_decode(qf, scale, unzigzag=bool(zz)))
+            if rgb:
+                want = O.ycbcr2rgb(want)
+            assert_bits(out[f], want, f"decode image C={C} zz={zz} rgb={rgb} scale={scale} f={f}")
+    assert L.ivc_intra_decode_image(N.ptr(q), F, H, W, 2, N.ptr(t), zz, rgb, N.ptr(out)) == N.E_SHAPE
+    assert L.ivc_intra_decode_image(N.ptr(q), F, H, 12, C, N.ptr(t), zz, rgb, N.ptr(out)) == N.E_SHAPE
+
+
+def test_symbols2image_stream_errors_match_reference():
+    """IntraCodec.symbols2image on the device raises what the reference's chain raises for a
+    malformed stream (ZeroRunCoder.decode, zerorun.py:46-88): a block overflowing 64, a
+    stream ending inside a block, right after a zero, or with too few blocks; trailing symbols
+    after the last expected block are ignored."""
+    from ivclab_amd.image import IntraCodec
+    codec = IntraCodec(quantization_scale=1.0)
+    rng = np.random.default_rng(5)
+    img = rng.integers(0, 256, (16, 24)).astype(np.uint8)
+    sym = np.asarray(codec.image2symbols(img, is_source_rgb=False))
+    shape = (16, 24, 3)
+    good = codec.symbols2image(sym, shape)
+    assert_bits(good, _chain_image(sym, shape, 1.0), "clean stream")
+    assert_bits(codec.symbols2image(np.concatenate([sym, [0, 0, 7]]).astype(np.int32), shape), good,
+                "trailing symbols ignored")
+    bad = {
+        "overflow": np.concatenate([[0, 70], sym]).astype(np.int64),
+        "ends_inside": sym[:-1],
+        "ends_after_zero": np.array([3, 0]),
+        "too_few": sym[: np.flatnonzero(sym == 4000)[2] + 1],
+    }
+    for name, s in bad.items():
+        with pytest.raises(Exception) as got:
+            codec.symbols2image(s, shape)
+        with pytest.raises(Exception) as want:
+            O.zerorun_decode(list(s), (2, 3, 3))
+        assert type(got.value) is type(want.value), (name, got.value, want.value)
+        if not isinstance(want.value, IndexError):
+            assert str(got.value) == str(want.value), name
 
 
 def test_intracodec_encode_decode_roundtrip():

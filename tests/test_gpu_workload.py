@@ -54,6 +54,51 @@ def test_inter_encode_sr16_1080p_across_s2_chunks():
     assert m.min() >= 0 and m.max() < (2 * sr + 1) ** 2
 
 
+def test_inter_encode_sr16_8k_chunks():
+    """cfg5's chain at its own frame size (BASELINE configs[4], 7680x4320): one 8K S2 plane is
+    132.7 MB, so the 256 MiB S2 chunk holds TWO frame pairs (at 1080p it holds 32) and the
+    search loop alternates pre-pass and tiled search every two pairs (ivc_motion.hip
+    launch_motion_estimate).  4 frames of the bench's cfg5 sequence (3 pairs = a full chunk of
+    2 and a remainder chunk of 1): mv and q of the top, middle and bottom
+    block-row stripes of every pair against the C oracle chain (motion.py:8-58,
+    patchquant.py:44-60); every pair written; and the chunked side-stream histograms of the
+    cfg5 step (1 pair per chunk) equal one call followed by main-stream histograms."""
+    import ivclab_amd._native as N
+    dev = torch.device("cuda:0")
+    F, H, W, sr = 4, 4320, 7680, 16
+    assert (256 << 20) // (H * W * 4) == 2              # pairs per S2 chunk at 8K
+    seq = bench.inter_frames(F, H, W, seed=5, dev=dev)
+    P, h = F - 1, H // 8
+    nmv = (2 * sr + 1) ** 2
+    mv = torch.full((P, h, W // 8), -1, dtype=torch.int64, device=dev)
+    q = torch.full((P, h, W // 8, 3, 64), -7, dtype=torch.int32, device=dev)
+    D.inter_encode(seq, sr, TABLE, mv, q)
+    hist1 = torch.zeros(bench.HIST_BINS + nmv, dtype=torch.int64, device=dev)
+    D.histogram(q.view(-1), bench.HIST_LO, hist1[:bench.HIST_BINS])
+    D.histogram(mv.view(-1), 0, hist1[bench.HIST_BINS:])
+    torch.cuda.synchronize()
+    host = seq.cpu().numpy()
+    for p in range(P):
+        for rows in ((0, 3), (h // 2 - 1, h // 2 + 2), (h - 3, h)):
+            wmv, wq = c_inter_encode(host[p], host[p + 1], sr, 1.0, rows=rows)
+            assert_bits(mv[p, rows[0]:rows[1]].cpu().numpy(), wmv[..., 0], f"mv pair {p} rows {rows}")
+            assert_bits(q[p, rows[0]:rows[1]].cpu().numpy(),
+                        wq.reshape(rows[1] - rows[0], W // 8, 3, 64), f"q pair {p} rows {rows}")
+    m = mv.cpu().numpy()
+    assert m.min() >= 0 and m.max() < nmv
+    assert int((q == -7).all(dim=-1).sum().item()) == 0   # no block left unwritten
+    # the cfg5 step itself (bench.make_sharded_step): 1 pair per chunk, side-stream histograms
+    mv2, q2 = torch.empty_like(mv), torch.empty_like(q)
+    hist2 = torch.zeros_like(hist1)
+    step = bench.make_sharded_step(D, N, seq, P, sr, TABLE, mv2, q2, hist2, 1, 2, False,
+                                   torch.cuda.Stream(device=dev))
+    step()
+    torch.cuda.synchronize()
+    assert torch.equal(mv2, mv) and torch.equal(q2, q)
+    assert_bits(hist2.cpu().numpy(), hist1.cpu().numpy(), "chunked side-stream histograms")
+    assert int(hist1[:bench.HIST_BINS].sum().item()) == q.numel()
+
+
 def test_inter_encode_sr16_zigzag_and_motion_range():
     """The zig-zag variant of the same chain on a sequence whose motion spans the whole
     +-16 window (large shifts, flat and textured regions), 4 pairs checked whole."""
@@ -95,6 +140,45 @@ def test_intra_encode_batch_past_4gib():
         assert_bits(out[f].cpu().numpy(), want, f"frame {f}")
     # the sentinel is outside every quantised value's range: nothing left unwritten
     assert int((out == -(1 << 30)).sum().item()) == 0
+
+
+def test_decode_batch_48_4k_frames():
+    """The decode chain at workload size (IntraCodec.symbols2image, intracodec.py:84-146):
+    48 4K frames encoded by the fused intra kernel with zig-zag ([48, 270, 480, 3, 64] int32,
+    4.78 GB), then (a) ivc_intra_decode_image of the coefficients and (b) the full device chain
+    from the frames' zero-run symbol stream (ivc_symbols2image_dev: zero-run decode ->
+    un-zig-zag -> dequantise -> IDCT -> unpatch -> ycbcr2rgb) into [48, 2160, 3840, 3] float64
+    (9.6 GB).  Frames 0, 23, 24, 47 are checked whole against the oracle (O.intra_decode,
+    unpatch, ycbcr2rgb)."""
+    dev = torch.device("cuda:0")
+    F, H, W = 48, 2160, 3840
+    frames = bench.intra_frames(F, H, W, seed=3, dev=dev).view(F, H, W, 1)
+    q = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+    D.intra_encode(frames, TABLE, q, zigzag=True)
+    out = torch.full((F, H, W, 3), float("nan"), dtype=torch.float64, device=dev)
+    D.intra_decode_image(q, TABLE, out, unzigzag=True, to_rgb=False)
+    torch.cuda.synchronize()
+    picks = (0, 23, 24, F - 1)
+    for f in picks:
+        want = O.unpatch(O.intra_decode(q[f].cpu().numpy(), 1.0, unzigzag=True))
+        assert_bits(out[f].cpu().numpy(), want, f"decoded frame {f}")
+    # (b) from the symbol stream, RGB
+    nblk = q.numel() // 64
+    offs = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
+    probe = torch.empty(1, dtype=torch.int32, device=dev)
+    D.zerorun_encode(q.view(nblk, 64), offs, probe)
+    sym = torch.empty(int(offs[-1].item()), dtype=torch.int32, device=dev)
+    D.zerorun_encode(q.view(nblk, 64), offs, sym)
+    del q, offs
+    err = torch.full((3,), -1, dtype=torch.int64, device=dev)
+    out.fill_(float("nan"))
+    D.symbols2image(sym, 3, TABLE, out, err, to_rgb=True)
+    torch.cuda.synchronize()
+    assert err.tolist() == [0, 0, 0]
+    for f in picks:
+        qf = O.intra_encode(frames[f].cpu().numpy(), 1.0, zigzag=True)
+        want = O.ycbcr2rgb(O.unpatch(O.intra_decode(qf, 1.0, unzigzag=True)))
+        assert_bits(out[f].cpu().numpy(), want, f"symbols2image frame {f}")
 
 
 def test_chunked_inter_encode_with_side_stream_histograms():
