@@ -12,6 +12,8 @@ libivc.so build, or null), `cpu_baseline` times the reference's algorithm (oracl
 
 Also reported from the same run (each with its own timing; none of them is `value`):
   zerorun / image2symbols  ZeroRunCoder on the zig-zag output, and pixels -> symbols fused
+  luma_only                the luma-table plane alone (5 B/px; not the reference's 3-plane
+                           output, so never `value`)
   decode                   IntraCodec.symbols2image of that stream on the device (zero-run
                            decode -> dequantise -> IDCT -> unpatch -> ycbcr2rgb), HBM roofline
                            of the coefficient-to-image kernel
@@ -509,6 +511,47 @@ def leg_intra(args, dist, rank, world, dev, table, result, verify):
     return frames, out
 
 
+def leg_luma_only(args, dist, rank, world, dev, table, frames, result, verify):
+    """The luma-table plane alone (SURVEY §8d's 5 B/px variant: 1 B u8 in + 4 B int32 out per
+    pixel).  Reported beside the headline, never `value`: the reference's PatchQuant.quantize
+    broadcasts a C = 1 image to 3 planes (patchquant.py:59), which the headline reproduces."""
+    import ivclab_amd.device as D
+    from ivclab_amd import _native as N
+    F, H, W = frames.shape[:3]
+    lum = torch.empty((F, H // 8, W // 8, 64), dtype=torch.int32, device=dev)
+    L = N.lib()
+
+    def step():
+        D.intra_encode_luma(frames, table, lum)
+
+    for _ in range(args.pace_calibrate):
+        step()
+        torch.cuda.synchronize()
+    N.check(L.ivc_store_pace_settle(PACE_MARGIN))
+    wall, ms = timed(dist, step, args.steps, args.warmup, sync_warmup=True)
+    algo = F * H * W * 5
+    result["luma_only"] = {
+        "metric": "Mpixels/s: 4K intra DCT+quant, luma-table plane only (not the reference's 3-plane output)",
+        "value": round(world * F * H * W * args.steps / wall / 1e6, 1), "unit": "Mpixels/s",
+        "ms_per_step": round(wall / args.steps * 1e3, 3),
+        "roofline": {"bound": "hbm", "kernel": "fused_encode_kernel<u8,f64,C=1,OUT_LUMA>",
+                     "kernel_ms": round(ms, 4), "achieved": round(algo / (ms * 1e-3) / 1e9, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "algorithmic_bytes_per_launch": algo,
+                     "store_pace": N.pace_stats(2)},
+    }
+    if verify is not None:
+        torch.cuda.synchronize()
+        from oracle import ivc_oracle as O
+        for f in sorted({0, F - 1}):
+            want = O.intra_encode(frames[f].cpu().numpy(), 1.0)[:, :, 0].reshape(H // 8, W // 8, 64)
+            check_equal(lum[f].cpu().numpy(), want, f"luma-only frame {f}", verify["failures"])
+        verify["checked"].append(f"luma_only: frames [0, {F - 1}] whole vs oracle plane 0")
+    del lum
+    torch.cuda.empty_cache()
+
+
 def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify):
     import ivclab_amd.device as D
     from ivclab_amd.distributed import global_bounds, global_histogram
@@ -730,14 +773,17 @@ def leg_class_api(args, dev, result, verify):
             return zz.flatten(pq.quantize(dct.transform(pt.patch(img))))
 
         def one_call():
-            o = np.empty((1, H // 8, W // 8, 3, 64), np.int32)
+            # the result array in the library's pinned host pool, as the drop-in classes
+            # allocate theirs (ivclab_amd._native.empty): one DMA, no staging copy
+            o = N.empty((1, H // 8, W // 8, 3, 64), np.int32)
             N.check(N.lib().ivc_intra_encode(N.ptr(np.ascontiguousarray(img[None])), 1, 1, H, W, C,
                                              N.ptr(t), N.F64, 1, N.ptr(o)))
             return o
 
         res = {}
-        for label, fn, reps in (("classes", classes, 3), ("one_call", one_call, 5)):
+        for label, fn, reps in (("classes", classes, 5), ("one_call", one_call, 5)):
             fn()
+            fn()            # second warm-up: the pinned pool holds a block per live result
             t0 = time.perf_counter()
             for _ in range(reps):
                 r = fn()
@@ -754,8 +800,10 @@ def leg_class_api(args, dev, result, verify):
         verify["checked"].append("class_api: every timed output vs oracle")
     result["class_api"] = dict(out, note="host NumPy in -> host NumPy out, PCIe included "
                                          "(DCT.transform -> PatchQuant.quantize -> ZigZag.flatten "
-                                         "as separate calls, or the fused ivc_intra_encode); "
-                                         "not comparable with the device-resident `value`")
+                                         "as separate calls, or the fused ivc_intra_encode); results "
+                                         "in the library's pinned host pool, inputs staged through "
+                                         "its pinned ring; not comparable with the device-resident "
+                                         "`value`")
 
 
 def make_sharded_step(D, N, seq, pairs, sr, table, mv, q, hist, chunk, hist_wg, zigzag, side):
@@ -889,6 +937,7 @@ def parse(argv=None):
     ap.add_argument("--no-symbols", action="store_true", help="skip the zero-run/exchange legs")
     ap.add_argument("--no-f64", action="store_true", help="skip the float64 ME leg")
     ap.add_argument("--no-decode", action="store_true", help="skip the symbols2image leg")
+    ap.add_argument("--no-luma", action="store_true", help="skip the luma-only (5 B/px) leg")
     ap.add_argument("--no-class-api", action="store_true", help="skip the host-buffer leg")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-sharded", action="store_true", help="skip the cfg5 8K leg")
@@ -936,6 +985,8 @@ def main():
     if args.no_intra:
         args.frames = 1
     frames, out = leg_intra(args, dist, rank, world, dev, table, result, verify)
+    if not args.no_luma:
+        leg_luma_only(args, dist, rank, world, dev, table, frames, result, verify)
     if not args.no_symbols:
         sym = leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify)
         if not args.no_decode:

@@ -58,6 +58,11 @@ int ivc_set_device(int device);
 int ivc_device_ok(void);
 /* release the library's cached scratch buffers on the current device */
 int ivc_release_scratch(void);
+/* Page-locked host memory for the host-buffer entry points' arrays: a transfer from or to a
+ * block of ivc_host_alloc is one DMA (no staging copy); freed blocks are cached by size and
+ * reused.  NULL when the runtime cannot pin more memory.                                   */
+void* ivc_host_alloc(int64_t bytes);
+int ivc_host_free(void* p);
 /* Store pacing of the fused coefficient encoders (ivc_intra_encode*, ivc_inter_encode*):
  * persistent waves release their output stores on the chip-wide clock so that the stores
  * in flight sweep the output in address order.  The rate is the total HBM
@@ -71,7 +76,7 @@ int ivc_set_store_pace(double total_gbps);
 double ivc_store_pace(void);
 double ivc_store_pace_late(void);
 /* Measurement statistics of the current device's paced launches since the last reset
- * (encoder 0 = image source, 1 = inter residual), folding every completed launch first:
+ * (encoder 0 = image source, 1 = inter residual, 2 = luma-only image), folding every completed launch first:
  * out[0] launches measured, [1] launches over the late threshold, [2] mean and [3] maximum
  * late fraction, [4] current rate (GB/s), [5] last late fraction, [6] mean achieved GB/s of
  * the measured launches (bytes / event time), [7] measurements still in flight, [8] launches
@@ -149,6 +154,13 @@ int ivc_intra_encode(const void* img, int dtype, int64_t nframes, int64_t H, int
 int ivc_intra_encode_dev(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                          int C, const double* table, int calc_dtype, int zigzag, int32_t* out,
                          int64_t* hist, int32_t hist_lo, int32_t nbins, void* stream);
+
+/* The luma-table plane only of u8 grayscale frames [nframes][H][W]: out [nframes][H/8][W/8][64]
+ * int32 = plane 0 of ivc_intra_encode_dev's output (C = 1, float64 arithmetic).  Not a
+ * reference output (PatchQuant.quantize broadcasts C = 1 to the 3 table planes,
+ * patchquant.py:59): a reported variant that moves 5 instead of 13 bytes per pixel.        */
+int ivc_intra_encode_luma_dev(const uint8_t* img, int64_t nframes, int64_t H, int64_t W,
+                              const double* table, int zigzag, int32_t* out, void* stream);
 
 /* (un-zig-zag ->) dequantize -> DCT-III(ortho) of nblk blocks of 3 x 64 int32 symbols.
  * out: nblk x 3 x 8 x 8 float64 = DCT.inverse_transform(PatchQuant.dequantize(ZigZag.unflatten(q)))

@@ -41,6 +41,8 @@ _SIGS = {
     "ivc_set_device": ([_I], _I),
     "ivc_device_ok": ([], _I),
     "ivc_release_scratch": ([], _I),
+    "ivc_host_alloc": ([_L], _P),
+    "ivc_host_free": ([_P], _I),
     "ivc_set_store_pace": ([_ct.c_double], _I),
     "ivc_store_pace": ([], _ct.c_double),
     "ivc_store_pace_late": ([], _ct.c_double),
@@ -61,6 +63,7 @@ _SIGS = {
     "ivc_intra_encode": ([_P, _I, _L, _L, _L, _I, _P, _I, _I, _P], _I),
     "ivc_intra_encode_dev": ([_P, _I, _L, _L, _L, _I, _P, _I, _I, _P, _P, _ct.c_int32,
                               _ct.c_int32, _P], _I),
+    "ivc_intra_encode_luma_dev": ([_P, _L, _L, _L, _P, _I, _P, _P], _I),
     "ivc_intra_decode": ([_P, _L, _P, _I, _I, _P], _I),
     "ivc_intra_decode_dev": ([_P, _L, _P, _I, _I, _P, _P], _I),
     "ivc_intra_decode_image": ([_P, _L, _L, _L, _I, _P, _I, _I, _P], _I),
@@ -197,6 +200,39 @@ def pace_trace(encoder: int = 0, max_records: int = 256):
     n = lib().ivc_store_pace_trace(encoder, out.ctypes.data, max_records)
     check(min(n, 0), "pace_trace")
     return [[round(float(v), 4 if i in (1, 4, 6) else 1) for i, v in enumerate(r)] for r in out[:n]]
+
+
+_PINNED_MIN = 1 << 20
+
+
+def empty(shape, dtype) -> np.ndarray:
+    """np.empty in a page-locked block of the library's host pool (ivc_host_alloc) when the
+    array is large (>= 1 MiB): the device writes it with one DMA and no staging copy.  The
+    block returns to the pool when the array (and every view of it) is garbage collected.
+    Falls back to np.empty when no device library is usable or pinning fails."""
+    import weakref
+    dtype = np.dtype(dtype)
+    shape = tuple(int(d) for d in (shape if np.iterable(shape) else (shape,)))
+    count = int(np.prod(shape, dtype=np.int64))
+    nbytes = count * dtype.itemsize
+    if nbytes < _PINNED_MIN:
+        return np.empty(shape, dtype)
+    try:
+        L = lib()
+    except (ImportError, IvcError):
+        return np.empty(shape, dtype)
+    p = L.ivc_host_alloc(nbytes)
+    if not p:
+        return np.empty(shape, dtype)
+    buf = (_ct.c_char * nbytes).from_address(p)
+    fin = weakref.finalize(buf, L.ivc_host_free, p)
+    fin.atexit = False
+    return np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
+
+
+def empty_like(a) -> np.ndarray:
+    a = np.asarray(a)
+    return empty(a.shape, a.dtype)
 
 
 def table_arg(table: np.ndarray) -> np.ndarray:

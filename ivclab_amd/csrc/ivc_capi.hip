@@ -6,8 +6,13 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <condition_variable>
+#include <functional>
+#include <map>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "ivc_internal.h"
 
@@ -28,16 +33,121 @@ int fail_hip(hipError_t e, const char* what) {
 bool valid_dtype(int dt) { return dt >= IVC_U8 && dt <= IVC_F64; }
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// ---------------------------------------------------------------- host copies ----------
+// Host buffers handed to the library are pageable NumPy memory: hipMemcpy from or to them
+// runs at ~10 GB/s.  Large transfers instead go through a per-device ring of pinned chunks:
+// the CPU copies chunk k between the caller's buffer and a pinned slot (split over a small
+// thread pool) while the DMA engine moves chunk k - 1 (H2D) or k + 1 (D2H) at pinned speed.
+class CopyPool {
+ public:
+  static CopyPool& get() {
+    static CopyPool* p = new CopyPool;      // never destroyed: its detached workers block on it
+    return *p;
+  }
+  // memcpy of n bytes split over the pool's workers and the calling thread
+  void copy(void* dst, const void* src, size_t n) {
+    const size_t min_part = 1u << 20;
+    int parts = (int)std::min<size_t>(workers_.size() + 1, std::max<size_t>(1, n / min_part));
+    if (parts <= 1) {
+      memcpy(dst, src, n);
+      return;
+    }
+    const size_t step = (n / parts + 63) & ~(size_t)63;
+    std::unique_lock<std::mutex> lk(mu_);
+    int pending = 0;
+    for (int i = 1; i < parts; ++i) {
+      const size_t off = step * i;
+      if (off >= n) break;
+      const size_t len = std::min(step, n - off);
+      ++pending;
+      tasks_.push_back([=] { memcpy((char*)dst + off, (const char*)src + off, len); });
+    }
+    outstanding_ += pending;
+    lk.unlock();
+    cv_.notify_all();
+    memcpy(dst, src, std::min(step, n));
+    lk.lock();
+    done_cv_.wait(lk, [&] { return outstanding_ == 0; });
+  }
+
+ private:
+  CopyPool() {
+    unsigned hw = std::thread::hardware_concurrency();
+    const int nw = (int)std::max(1u, std::min(7u, hw > 2 ? hw / 2 - 1 : 1u));
+    for (int i = 0; i < nw; ++i) workers_.emplace_back([this] { run(); });
+    for (auto& t : workers_) t.detach();     // process-long (no join at exit)
+  }
+  void run() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return !tasks_.empty(); });
+        f = std::move(tasks_.back());
+        tasks_.pop_back();
+      }
+      f();
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--outstanding_ == 0) done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  std::vector<std::function<void()>> tasks_;
+  std::vector<std::thread> workers_;
+  int outstanding_ = 0;
+};
+
+// ---------------------------------------------------------------- pinned host blocks ---
+// ivc_host_alloc: page-locked host memory the drop-in classes allocate their NumPy results in
+// (ivclab_amd._native.empty).  A transfer between such a block and the device is one DMA at
+// full PCIe speed with no CPU copy and no first-touch page faults; freed blocks are cached by
+// size (up to kHostCacheMax) so repeated calls of the same shapes reuse them.
+std::mutex g_host_mu;
+std::map<uintptr_t, size_t> g_host_live;          // block start -> bytes
+std::multimap<size_t, void*> g_host_cache;        // freed blocks by size
+size_t g_host_cached = 0;
+constexpr size_t kHostCacheMax = 4ull << 30;
+constexpr size_t kHostGrain = 2u << 20;
+
+bool host_pinned(const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> g(g_host_mu);
+  const uintptr_t a = (uintptr_t)p;
+  auto it = g_host_live.upper_bound(a);
+  if (it == g_host_live.begin()) return false;
+  --it;
+  return a >= it->first && a + bytes <= it->first + it->second;
+}
+
 // ---------------------------------------------------------------- device context -------
 constexpr int kMaxDev = 64;
 constexpr int kSlots = 6;
+constexpr int kPinSlots = 4;
+constexpr size_t kPinChunk = 8u << 20;      // bytes per pinned slot
+constexpr size_t kPinMin = 1u << 20;        // smaller transfers go straight from pageable memory
 struct DevCtx {
   std::mutex mu;
   hipStream_t stream = nullptr;
   void* slot[kSlots] = {};
   size_t cap[kSlots] = {};
+  void* pin[kPinSlots] = {};
+  hipEvent_t pin_ev[kPinSlots] = {};
+  int pin_state = 0;                        // 0 untried, 1 ready, -1 unavailable
+  int pin_next = 0;
 };
 DevCtx g_ctx[kMaxDev];
+
+bool pinned_ready(DevCtx* c) {
+  if (c->pin_state == 0) {
+    c->pin_state = 1;
+    for (int i = 0; i < kPinSlots && c->pin_state == 1; ++i)
+      if (hipHostMalloc(&c->pin[i], kPinChunk, hipHostMallocDefault) != hipSuccess ||
+          hipEventCreateWithFlags(&c->pin_ev[i], hipEventDisableTiming) != hipSuccess)
+        c->pin_state = -1;                  // keep what was allocated; use the pageable path
+    (void)hipGetLastError();
+  }
+  return c->pin_state == 1;
+}
 
 int current_device(int* dev) {
   hipError_t e = hipGetDevice(dev);
@@ -83,10 +193,30 @@ struct Staging {
     }
     return ctx->slot[i];
   }
+  // next pinned slot, once the DMA that last used it has finished
+  int take_pin() {
+    const int k = ctx->pin_next;
+    ctx->pin_next = (k + 1) % kPinSlots;
+    hipError_t e = hipEventSynchronize(ctx->pin_ev[k]);
+    if (e != hipSuccess) status = fail_hip(e, "hipEventSynchronize");
+    return k;
+  }
   void* in(const void* host, size_t bytes) {
     void* d = alloc(bytes);
-    if (d && bytes) {
+    if (!d || !bytes) return d;
+    if (bytes < kPinMin || host_pinned(host, bytes) || !pinned_ready(ctx)) {
       hipError_t e = hipMemcpyAsync(d, host, bytes, hipMemcpyHostToDevice, ctx->stream);
+      if (e != hipSuccess) status = fail_hip(e, "hipMemcpyAsync H2D");
+      return d;
+    }
+    // CPU copy of chunk k into a pinned slot overlaps the DMA of chunk k - 1
+    for (size_t off = 0; off < bytes && !status; off += kPinChunk) {
+      const size_t n = std::min(kPinChunk, bytes - off);
+      const int k = take_pin();
+      if (status) break;
+      CopyPool::get().copy(ctx->pin[k], (const char*)host + off, n);
+      hipError_t e = hipMemcpyAsync((char*)d + off, ctx->pin[k], n, hipMemcpyHostToDevice, ctx->stream);
+      if (e == hipSuccess) e = hipEventRecord(ctx->pin_ev[k], ctx->stream);
       if (e != hipSuccess) status = fail_hip(e, "hipMemcpyAsync H2D");
     }
     return d;
@@ -99,11 +229,37 @@ struct Staging {
   }
   int out(void* host, const void* dev, size_t bytes) {
     if (status) return status;
-    if (bytes) {
+    if (!bytes) return IVC_OK;
+    if (bytes < kPinMin || host_pinned(host, bytes) || !pinned_ready(ctx)) {
       hipError_t e = hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream);
       if (e != hipSuccess) return status = fail_hip(e, "hipMemcpyAsync D2H");
+      return IVC_OK;
     }
-    return IVC_OK;
+    // up to kPinSlots DMAs in flight; the CPU drains chunk k into the caller's buffer while
+    // the DMA engine fills the next slots (synchronous: the data is in `host` on return)
+    const size_t nchunk = (bytes + kPinChunk - 1) / kPinChunk;
+    std::vector<int> slot_of(nchunk);
+    auto issue = [&](size_t c) {
+      const size_t off = c * kPinChunk, n = std::min(kPinChunk, bytes - off);
+      const int k = take_pin();
+      if (status) return;
+      slot_of[c] = k;
+      hipError_t e = hipMemcpyAsync(ctx->pin[k], (const char*)dev + off, n, hipMemcpyDeviceToHost,
+                                    ctx->stream);
+      if (e == hipSuccess) e = hipEventRecord(ctx->pin_ev[k], ctx->stream);
+      if (e != hipSuccess) status = fail_hip(e, "hipMemcpyAsync D2H");
+    };
+    size_t issued = 0;
+    for (; issued < nchunk && issued < (size_t)kPinSlots - 1 && !status; ++issued) issue(issued);
+    for (size_t c = 0; c < nchunk && !status; ++c) {
+      const int k = slot_of[c];
+      hipError_t e = hipEventSynchronize(ctx->pin_ev[k]);
+      if (e != hipSuccess) return status = fail_hip(e, "hipEventSynchronize");
+      const size_t off = c * kPinChunk, n = std::min(kPinChunk, bytes - off);
+      if (issued < nchunk) issue(issued++);   // reuses a slot already drained
+      CopyPool::get().copy((char*)host + off, ctx->pin[k], n);
+    }
+    return status;
   }
   int sync() {
     if (status) return status;
@@ -195,6 +351,40 @@ int ivc_device_ok(void) {
   return strncmp(p.gcnArchName, "gfx950", 6) == 0 ? 1 : 0;
 }
 
+void* ivc_host_alloc(int64_t bytes) {
+  if (bytes <= 0) return nullptr;
+  const size_t n = ((size_t)bytes + kHostGrain - 1) / kHostGrain * kHostGrain;
+  std::lock_guard<std::mutex> g(g_host_mu);
+  void* p = nullptr;
+  auto it = g_host_cache.find(n);
+  if (it != g_host_cache.end()) {
+    p = it->second;
+    g_host_cache.erase(it);
+    g_host_cached -= n;
+  } else if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  g_host_live[(uintptr_t)p] = n;
+  return p;
+}
+
+int ivc_host_free(void* p) {
+  if (!p) return IVC_OK;
+  std::lock_guard<std::mutex> g(g_host_mu);
+  auto it = g_host_live.find((uintptr_t)p);
+  if (it == g_host_live.end()) return fail(IVC_E_ARG, "ivc_host_free: not a block of ivc_host_alloc");
+  const size_t n = it->second;
+  g_host_live.erase(it);
+  if (g_host_cached + n <= kHostCacheMax) {
+    g_host_cache.emplace(n, p);
+    g_host_cached += n;
+  } else {
+    (void)hipHostFree(p);
+  }
+  return IVC_OK;
+}
+
 int ivc_set_store_pace(double total_gbps) {
   if (!(total_gbps >= 0)) return fail(IVC_E_ARG, "ivc_set_store_pace: rate must be >= 0");
   set_store_pace_gbps(total_gbps);
@@ -206,8 +396,8 @@ double ivc_store_pace(void) { return store_pace_gbps(); }
 double ivc_store_pace_late(void) { return store_pace_late_fraction(); }
 
 int ivc_store_pace_stats(int encoder, double* out, int n) {
-  if (encoder < 0 || encoder > 1 || n < 0 || (n > 0 && !out))
-    return fail(IVC_E_ARG, "ivc_store_pace_stats: encoder must be 0 or 1, out must hold n values");
+  if (encoder < 0 || encoder > 2 || n < 0 || (n > 0 && !out))
+    return fail(IVC_E_ARG, "ivc_store_pace_stats: encoder must be 0, 1 or 2, out must hold n values");
   return store_pace_stats(encoder, out, n);
 }
 
@@ -217,8 +407,8 @@ int ivc_store_pace_reset_stats(void) {
 }
 
 int ivc_store_pace_trace(int encoder, double* out, int max_records) {
-  if (encoder < 0 || encoder > 1 || max_records < 0 || (max_records > 0 && !out))
-    return fail(IVC_E_ARG, "ivc_store_pace_trace: encoder must be 0 or 1, out must hold "
+  if (encoder < 0 || encoder > 2 || max_records < 0 || (max_records > 0 && !out))
+    return fail(IVC_E_ARG, "ivc_store_pace_trace: encoder must be 0, 1 or 2, out must hold "
                            "7 * max_records values");
   return store_pace_trace(encoder, out, max_records);
 }
@@ -399,6 +589,16 @@ int ivc_intra_encode(const void* img, int dtype, int64_t nframes, int64_t H, int
                                       st.ctx->stream), "intra_encode"));
   TRY(st.out(out, d_out, ob));
   return st.sync();
+}
+
+int ivc_intra_encode_luma_dev(const uint8_t* img, int64_t nframes, int64_t H, int64_t W,
+                              const double* table, int zigzag, int32_t* out, void* stream) {
+  TRY(check_frames(nframes, H, W, "intra_encode_luma"));
+  CHECK(aligned16(img) && aligned16(out), IVC_E_ARG, "intra_encode_luma_dev: pointers must be 16-byte aligned");
+  QTab t;
+  TRY(load_table(table, &t));
+  return dev_launch(launch_intra_encode_luma(img, nframes, H, W, t, zigzag, out, (hipStream_t)stream),
+                    "intra_encode_luma");
 }
 
 int ivc_intra_decode_dev(const int32_t* q, int64_t nblk, const double* table, int calc_dtype,

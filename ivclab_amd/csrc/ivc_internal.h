@@ -36,6 +36,8 @@ hipError_t launch_zigzag(const void* src, int64_t nrow, int64_t stride, int esiz
 hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                                int C, const QTab& t, int calc_dtype, int zigzag, int32_t* out,
                                hipStream_t s);
+hipError_t launch_intra_encode_luma(const uint8_t* img, int64_t nframes, int64_t H, int64_t W,
+                                    const QTab& t, int zigzag, int32_t* out, hipStream_t s);
 // decode chain (ivc_decode.hip): [nblk][3][64] -> [nblk][3][8][8] f64, and
 // [F][h][w][C][64] -> [F][H][W][3] f64 image (optionally ycbcr2rgb)
 hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, int unzigzag,

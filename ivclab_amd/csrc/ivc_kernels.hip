@@ -564,11 +564,24 @@ __device__ __forceinline__ void gather_inter(const FusedArgs& a, uint32_t lt, in
 
 // The staged group (LDS, block pitch OS_PITCH) leaves as 6 x 1 KiB buffer_store_dwordx4;
 // lanes past a ragged group's edge, or a non-existent group, fall outside the descriptor.
-template <int NG, int C, bool DUP>
+template <int NG, int C, bool DUP, bool LUMA = false>
 __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* os, int lane,
                                             uint32_t lt, int g, bool exists) {
   constexpr int PITCH = os_pitch<C, DUP>();
   const GroupLoc L = group_loc<NG>(a, lt, g);
+  if constexpr (LUMA) {     // plane 0 only: 2 x 1 KiB
+    const __amdgpu_buffer_rsrc_t rl =
+        make_rsrc(a.out + (((int64_t)L.f * a.h + L.bi) * a.w + L.bj0) * 64,
+                  exists ? (uint32_t)L.nb * 256u : 0u);
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int ch = lane + 64 * jj;
+      const int4 val = *reinterpret_cast<const int4*>(os + (ch >> 4) * PITCH + (ch & 15) * 4);
+      const u32x4 w4 = {(uint32_t)val.x, (uint32_t)val.y, (uint32_t)val.z, (uint32_t)val.w};
+      __builtin_amdgcn_raw_buffer_store_b128(w4, rl, ch * 16, 0, IVC_STORE_AUX);
+    }
+    return;
+  }
   const __amdgpu_buffer_rsrc_t ro =
       make_rsrc(a.out + (((int64_t)L.f * a.h + L.bi) * a.w + L.bj0) * 192,
                 exists ? (uint32_t)L.nb * 768u : 0u);
@@ -587,11 +600,13 @@ __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* o
 // Output modes of the fused kernel: the quantised blocks themselves (OUT_COEFS: staged in LDS
 // and stored), or the blocks' zero-run symbols (ivclab/entropy/zerorun.py:10-43) — their
 // per-group counts (OUT_COUNT) or the symbol stream at scanned offsets (OUT_SYMBOLS).
-enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2 };
+// OUT_LUMA: the luma-table plane only ([F][h][w][64], 4 B/px out instead of the reference's
+// 12 B/px 3-plane broadcast) — a reported variant, not the reference's output.
+enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2, OUT_LUMA = 3 };
 
 // Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging.
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
-          bool DUP>
+          bool DUP, bool LUMA = false>
 __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI, C, SRC>& v,
                                              T* xs, int32_t* os, const double* srq, const D* sq,
                                              int b, int r, uint32_t zp0, uint32_t zp1) {
@@ -644,6 +659,7 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
 #pragma unroll
     for (int pi = 0; pi < (C == 1 ? 3 : 1); ++pi) {
       if (C == 1 && DUP && pi == 2) break;  // plane 2 == plane 1: stored from plane 1
+      if (LUMA && pi > 0) break;
       const int p = C == 1 ? pi : c;
       int32_t* ob = os + b * os_pitch<C, DUP>() + p * 64;
       auto pos_of = [&](int i) {
@@ -905,7 +921,10 @@ __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b,
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
           int NG, bool DUP, int OUTM = OUT_COEFS>
 __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) {
-  static_assert(OUTM == OUT_COEFS || (ZZ && SRC == SRC_IMAGE), "symbols need zig-zag order");
+  static_assert(OUTM == OUT_COEFS || OUTM == OUT_LUMA || (ZZ && SRC == SRC_IMAGE),
+                "symbols need zig-zag order");
+  static_assert(OUTM != OUT_LUMA || C == 1, "the luma-only output is for C = 1 images");
+  constexpr bool COEF = OUTM == OUT_COEFS || OUTM == OUT_LUMA;
   typedef WaveLds<T, C, DUP> L;
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
   __shared__ double srq[FAST ? 192 : 1];
@@ -937,7 +956,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
 
   // pacing clock of this wave's slots (slot = groups stored so far), in 1/256 ticks
   uint64_t pace_next = 0;
-  if (OUTM == OUT_COEFS && a.pace_d) {
+  if (COEF && a.pace_d) {
     pace_next = (*a.pace_t0 << 8) + (uint64_t)a.pace_d * (blockIdx.x * 4u + wave) / nwaves;
     if (tid == 0)
       __hip_atomic_fetch_min(reinterpret_cast<unsigned long long*>(a.pace_t0) + PACE_START,
@@ -948,7 +967,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
   // dispatched and the first tiles loaded while the schedule runs) and of the rest
   uint32_t nlate_early = 0, nlate = 0, pslot = 0, first_late = 0xffffffffu;
   auto store_prev = [&](uint32_t plt, int pg, bool have_prev) {
-    if constexpr (OUTM == OUT_COEFS) {
+    if constexpr (COEF) {
       if (a.pace_d && have_prev) {
         const uint32_t l = pace_until(pace_next, a.pace_d);
         if (pslot < a.pace_early) {
@@ -960,7 +979,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
         ++pslot;
         pace_next += a.pace_d;
       }
-      store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+      store_group<NG, C, DUP, OUTM == OUT_LUMA>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
     }
   };
   uint32_t plt = 0;
@@ -999,8 +1018,8 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
           store_prev(plt, pg, have_prev);
           RowReg<TI, C, SRC> v;
           group_row<TI, C, NG>(ring[p], g, lane, v);
-          encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
-          if constexpr (OUTM != OUT_COEFS) {
+          encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+          if constexpr (!COEF) {
             if (ex) zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, tp, g).nb, (int64_t)tp * NG + g);
           }
           plt = tp;
@@ -1020,9 +1039,9 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
     TileRaw<TI, C, NG> raw;
     if constexpr (SRC == SRC_IMAGE) {
       load_tile<TI, C, NG>(a, lt, lt < nlt, lane, raw);
-      if constexpr (OUTM == OUT_COEFS) {
+      if constexpr (COEF) {
 #pragma unroll
-        for (int g = 1; g < NG; ++g) store_group<NG, C, DUP>(a, os, lane, 0u, 0, false);
+        for (int g = 1; g < NG; ++g) store_group<NG, C, DUP, OUTM == OUT_LUMA>(a, os, lane, 0u, 0, false);
       }
     }
     for (; lt < nlt; lt += nwaves) {
@@ -1040,8 +1059,8 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
         } else {
           gather_inter(a, lt, b, r, v);
         }
-        encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
-        if constexpr (OUTM != OUT_COEFS)
+        encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+        if constexpr (!COEF)
           zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, lt, g).nb, (int64_t)lt * NG + g);
         plt = lt;
         pg = g;
@@ -1050,7 +1069,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
       if constexpr (SRC == SRC_IMAGE) raw = nraw;
     }
   }
-  if constexpr (OUTM == OUT_COEFS) {
+  if constexpr (COEF) {
     if (a.pace_d && have_prev) {
       const uint32_t l = pace_until(pace_next, a.pace_d);
       if (pslot < a.pace_early) {
@@ -1060,7 +1079,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
         if (l && first_late == 0xffffffffu) first_late = pslot;
       }
     }
-    store_group<NG, C, DUP>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
+    store_group<NG, C, DUP, OUTM == OUT_LUMA>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
     if ((nlate | nlate_early) && lane == 0) {
       unsigned long long* blk = reinterpret_cast<unsigned long long*>(a.pace_t0);
       __hip_atomic_fetch_add(blk + 1 + blockIdx.x % PACE_SHARDS,
@@ -1155,8 +1174,21 @@ static double g_pace_start = -1.0;
 // late-slot fractions are bimodal: < 1% below the device's rate, 20-50% once over it
 constexpr double PACE_LATE_HI = 0.05, PACE_MAX_GBPS = 7600.0;
 constexpr int PACE_RING = 32, PACE_TRACE = 256;
-// lead of the schedule origin over the stamp kernel's clock read (ticks of 10 ns)
-constexpr uint32_t PACE_LEAD = 300;
+// Lead of the schedule origin over the stamp kernel's clock read (ticks of 10 ns).  The
+// kernel's first workgroups enter ~5 us after the stamp, and a wave needs ~20 us (its first
+// tile loads, first groups) before its first store: with the origin at +3 us the first ~10 %
+// of every wave's slots ran late (20-48 % of them) and the late waves' out-of-order stores
+// cost 4 % of the launch; with +30 us no start-up slot is late (same-box A/B over leads of
+// 3, 15, 30, 50, 80, 120 and 200 us, tools/gpu_r03_lead.sh: 4.968 -> 4.717 ms; past 50 us the
+// idle wait costs more than it saves).  IVC_PACE_LEAD overrides it (experiments).
+static uint32_t pace_lead() {
+  static const uint32_t v = [] {
+    const char* e = getenv("IVC_PACE_LEAD");
+    const long x = e ? atol(e) : 3000;
+    return (uint32_t)(x < 0 ? 0 : (x > 1000000 ? 1000000 : x));
+  }();
+  return v;
+}
 
 enum PaceSlotState { PS_FREE = 0, PS_ARMED, PS_CLOSED, PS_VOID };
 struct PaceSlot {
@@ -1165,6 +1197,7 @@ struct PaceSlot {
   hipEvent_t done = nullptr;      // after the pace block's copy
   double slots = 0, slots_per_wave = 0, bytes = 0, rate = 0;
   int state = PS_FREE;
+  int64_t gen = 0;                // the controller generation it was launched under
 };
 struct PaceStats {
   int64_t measured = 0, over = 0, late_fast = 0;
@@ -1188,9 +1221,10 @@ struct PaceState {
   PaceStats st;
   PaceTraceRec trace[PACE_TRACE];
   int64_t ntrace = 0;             // records since the last reset (ring of PACE_TRACE)
+  int64_t gen = 0;                // bumped by ivc_set_store_pace: older launches are not folded
 };
-// per device and per encoder (0: image source, 1: inter residual source)
-static PaceState g_pace[64][2];
+// per device and per encoder (0: image source, 1: inter residual source, 2: luma-only image)
+static PaceState g_pace[64][3];
 
 static double pace_start_rate() {
   if (g_pace_start < 0) {
@@ -1269,10 +1303,9 @@ static void pace_harvest(PaceState& P) {
     PaceSlot& S = P.ring[P.head];
     if (S.state == PS_ARMED) break;
     if (S.state == PS_CLOSED) {
-      if (P.rate > 0) {
-        if (hipEventQuery(S.done) != hipSuccess) break;
-        pace_fold(P, S);
-      }                            // else: pacing switched off since, drop the measurement
+      if (hipEventQuery(S.done) != hipSuccess) break;   // its copy may still land in S.host
+      // dropped when pacing was switched off or the rate set anew since its launch
+      if (P.rate > 0 && S.gen == P.gen) pace_fold(P, S);
     }
     S.state = PS_FREE;
     P.head = (P.head + 1) % PACE_RING;
@@ -1348,7 +1381,7 @@ void store_pace_reset_stats() {
 
 void store_pace_settle(double margin) {
   std::lock_guard<std::mutex> g(g_pace_mu);
-  for (int kind = 0; kind < 2; ++kind) {
+  for (int kind = 0; kind < 3; ++kind) {
     PaceState* P = pace_state_current(kind);
     if (!P || !P->blk || P->rate <= 0) continue;
     pace_harvest(*P);
@@ -1366,6 +1399,7 @@ void set_store_pace_gbps(double gbps) {
       p.rate = g_pace_start;
       p.too_fast = 1e30;
       p.good_rate = p.good_gbps = 0;
+      p.gen += 1;                 // launches of the previous rate are never folded into this one
     }
 }
 
@@ -1387,7 +1421,7 @@ static bool pace_alloc(PaceState& P) {
 
 // Turns pacing on for a launch of `nwaves` persistent waves that store `slots` groups each
 // (of `group_bytes` input + output bytes): a one-lane kernel on the same stream stamps the
-// start time (the clock PACE_LEAD ahead, covering the launch gap) and clears the counters.
+// start time (the clock pace_lead() ticks ahead, covering the launch gap) and clears the counters.
 // Returns the reserved measurement slot (-1: the launch is paced but not measured), which the
 // caller hands to finish_pacing after the kernel.  Concurrent launches on other streams may
 // overwrite the device's pace block between a stamp and its kernel; that only shifts a
@@ -1421,13 +1455,14 @@ static int setup_pacing(FusedArgs& a, int kind, int64_t nwaves, int64_t slots,
       S.slots_per_wave = (double)slots;
       S.bytes = (double)nwaves * (double)slots * group_bytes;
       S.rate = P.rate;
+      S.gen = P.gen;
       S.state = PS_ARMED;
       P.count += 1;
       slot = k;
     }
     (void)hipGetLastError();
   }
-  pace_stamp_kernel<<<1, 1, 0, s>>>(P.blk, PACE_LEAD);
+  pace_stamp_kernel<<<1, 1, 0, s>>>(P.blk, pace_lead());
   a.pace_t0 = P.blk;
   a.pace_d = (uint32_t)d256;
   a.pace_early = (uint32_t)pace_early_slots((double)slots);
@@ -1452,7 +1487,7 @@ static void finish_pacing(int kind, int slot, hipStream_t s) {
 
 // NG: groups of 8 blocks per wave load (wide, whole-cache-line row loads for u8 luma)
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CM,
-          int NGW = IVC_WIDE_NG>
+          int NGW = IVC_WIDE_NG, int OUTM = OUT_COEFS>
 static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s) {
   constexpr int NG = (sizeof(TI) == 1 && C == 1 && SRC == SRC_IMAGE) ? NGW : 1;
   FusedArgs a = a_in;
@@ -1471,17 +1506,22 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
     }
   };
   // input + output bytes of one group (8 blocks)
-  const double gbytes = 8.0 * (SRC == SRC_INTER ? 64.0 * 2 + 8.0 + 768.0
-                                                : 64.0 * C * sizeof(TI) + 768.0);
+  const double out_bytes = OUTM == OUT_LUMA ? 256.0 : 768.0;
+  const double gbytes = 8.0 * (SRC == SRC_INTER ? 64.0 * 2 + 8.0 + out_bytes
+                                                : 64.0 * C * sizeof(TI) + out_bytes);
+  // pacing state per encoder: image source, inter residual, luma-only image
+  const int kind = OUTM == OUT_LUMA ? 2 : SRC;
   auto go = [&](auto k) {
     const unsigned g = grid(k);
     const int64_t nw = 4 * (int64_t)g;
-    const int slot = setup_pacing(a, SRC, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
+    const int slot = setup_pacing(a, kind, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
     k<<<g, 256, 0, s>>>(a, t);
-    finish_pacing(SRC, slot, s);
+    finish_pacing(kind, slot, s);
   };
-  if (C == 1 && a.dup12) go(fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, C == 1>);
-  else go(fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, false>);
+  if (C == 1 && (a.dup12 || OUTM == OUT_LUMA))
+    go(fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, C == 1, OUTM>);
+  else
+    go(fused_encode_kernel<TI, T, D, C, FAST, ZZ, SRC, CM, NG, false, OUTM>);
 }
 
 // The FAST quotient check needs |quotient| < 2^20.  Integer pixels
@@ -1562,6 +1602,23 @@ hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int6
     default:
       return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// The luma-table plane only of a u8 C = 1 batch: out [F][h][w][64] int32 (plane 0 of what
+// launch_intra_encode writes).  A reported variant (5 B/px of HBM traffic instead of 13): the
+// reference's PatchQuant.quantize broadcasts C = 1 to 3 planes (patchquant.py:59).
+hipError_t launch_intra_encode_luma(const uint8_t* img, int64_t nframes, int64_t H, int64_t W,
+                                    const QTab& t, int zigzag, int32_t* out, hipStream_t s) {
+  if (nframes <= 0 || H <= 0 || W <= 0) return hipSuccess;
+  FusedArgs a = make_fused_args(img, nullptr, out, nframes, H, W, 0, t);
+  if (nframes * (int64_t)a.h * a.tpr >= (1LL << 31)) return hipErrorInvalidValue;
+  const bool cm = needs_magnitude_check(t);
+#define LUMA_GO(ZZV, CMV) \
+  launch_fused_one<uint8_t, double, double, 1, true, ZZV, SRC_IMAGE, CMV, IVC_WIDE_NG, OUT_LUMA>(a, t, s)
+  if (zigzag) { if (cm) LUMA_GO(true, true); else LUMA_GO(true, false); }
+  else { if (cm) LUMA_GO(false, true); else LUMA_GO(false, false); }
+#undef LUMA_GO
   return hipGetLastError();
 }
 

@@ -185,3 +185,22 @@ def symbols2image(sym, C, table, out, err, eob=4000, to_rgb=False, stream=None):
     N.check(N.lib().ivc_symbols2image_dev(sym.data_ptr(), sym.numel(), F, H, W, int(C), N.ptr(t),
                                           int(eob), int(bool(to_rgb)), out.data_ptr(),
                                           err.data_ptr(), _stream(stream)), "symbols2image")
+
+
+def intra_encode_luma(frames, table, out, zigzag=False, stream=None):
+    """u8 frames [F, H, W] (or [F, H, W, 1]) -> out [F, H/8, W/8, 64] int32: plane 0 (the
+    luminance table) of intra_encode's output.  Not the reference's output (PatchQuant
+    broadcasts C = 1 to 3 planes, patchquant.py:59): a reported 5 B/px variant."""
+    import torch
+    _contig(frames, "frames"); _contig(out, "out")
+    if frames.dtype != torch.uint8 or out.dtype != torch.int32:
+        raise ValueError("intra_encode_luma: uint8 frames, int32 out")
+    if frames.dim() == 4 and frames.shape[3] != 1:
+        raise ValueError("intra_encode_luma: one channel")
+    F, H, W = frames.shape[:3]
+    if tuple(out.shape) != (F, H // 8, W // 8, 64):
+        raise ValueError(f"intra_encode_luma: out must be {(F, H // 8, W // 8, 64)}")
+    t = N.table_arg(table)
+    N.check(N.lib().ivc_intra_encode_luma_dev(frames.data_ptr(), F, H, W, N.ptr(t),
+                                              int(bool(zigzag)), out.data_ptr(), _stream(stream)),
+            "intra_encode_luma")

@@ -40,7 +40,8 @@ def stats_marg(image, pixel_range):
     / image.size, counted on the GPU.
 
     Integer images over unit-spaced integer edges (the symbol and pixel statistics of the
-    codec) take the integer histogram kernel on the raw values: np.histogram drops values
+    codec, including the int64 symbol / motion-vector arrays of the chapter-4 exercises) take
+    the integer histogram kernels on the raw values: np.histogram drops values
     outside [edges[0], edges[-1]] and closes the last bin; the kernel clamps, so two guard
     bins on each side absorb the out-of-range values and the top edge value is folded into
     the last bin.  Everything else — float images, any edges, an int bin count or a binning
@@ -53,19 +54,26 @@ def stats_marg(image, pixel_range):
     edges = np.asarray(pixel_range)
     unit_int = (edges.ndim == 1 and edges.size >= 2 and np.issubdtype(edges.dtype, np.integer)
                 and bool(np.all(np.diff(edges) == 1)))
-    # integers of up to 32 bits are exact in float64, so counting the raw values is the same
-    # as counting the reference's float64 casts; wider ones take the float path (the cast
-    # rounds beyond 2^53, as the reference's does)
-    small_int = (np.issubdtype(a.dtype, np.integer) and a.dtype.itemsize <= 4) or a.dtype == np.bool_
-    if unit_int and small_int:
+    # Integer data over unit-spaced integer edges inside (-2^53, 2^53): every value lands in the
+    # same bin before and after the reference's float64 cast (values within the edges are exact
+    # in float64; a value beyond +-2^53 casts to something beyond the edges either way), so the
+    # raw values are counted by the integer kernels (int32 when values and bins fit, else int64)
+    int_data = np.issubdtype(a.dtype, np.integer) or a.dtype == np.bool_
+    if unit_int and int_data and -2**53 < int(edges[0]) and int(edges[-1]) < 2**53 \
+            and edges.size - 1 + 3 <= np.iinfo(np.int32).max:
         lo, nb = int(edges[0]), edges.size - 1
         x = np.ascontiguousarray(a.ravel())
         hist = np.zeros(nb + 3, np.int64)              # [< lo | lo .. lo+nb-1 | lo+nb | > lo+nb]
-        if x.dtype != np.uint32:
+        i32 = np.iinfo(np.int32)
+        fits32 = (x.dtype == np.bool_ or (x.dtype.itemsize <= 4 and x.dtype != np.uint32)) \
+            and i32.min <= lo - 1 and lo + nb + 1 <= i32.max
+        if fits32:
             x32 = x.astype(np.int32, copy=False)
             N.check(N.lib().ivc_histogram_i32(N.ptr(x32), x32.size, lo - 1, nb + 3, N.ptr(hist)),
                     "stats_marg")
         else:
+            if x.dtype == np.uint64 and x.size and x.max() > np.iinfo(np.int64).max:
+                x = np.minimum(x, np.uint64(np.iinfo(np.int64).max))   # all beyond the edges
             x64 = x.astype(np.int64, copy=False)
             N.check(N.lib().ivc_histogram_i64(N.ptr(x64), x64.size, lo - 1, nb + 3, N.ptr(hist)),
                     "stats_marg")

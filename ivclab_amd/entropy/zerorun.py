@@ -80,7 +80,7 @@ class ZeroRunCoder:
                              h=h, w=w, c=c, p=B)
         if B > 64:
             raise NotImplementedError("ZeroRunCoder: block_size > 64 is not supported")
-        out = np.empty((expected, B), np.int32)
+        out = N.empty((expected, B), np.int32)
         err = np.zeros(3, np.int64)
         N.check(N.lib().ivc_zerorun_decode(N.ptr(sym), sym.size, expected, B, int(self.EOB),
                                            N.ptr(out), N.ptr(err)), "zerorun_decode")

@@ -80,7 +80,7 @@ class IntraCodec:
         """ivc_symbols2image: [h*8, w*8, 3] float64 (ycbcr, or RGB when to_rgb)."""
         sym, is_list = decode_input(symbols)
         t = N.table_arg(self.quant.get_quantization_table())
-        out = np.empty((h * 8, w * 8, 3), np.float64)
+        out = N.empty((h * 8, w * 8, 3), np.float64)
         err = np.zeros(3, np.int64)
         N.check(N.lib().ivc_symbols2image(N.ptr(sym), sym.size, 1, h * 8, w * 8, C, N.ptr(t),
                                           int(self.zerorun.EOB), int(bool(to_rgb)), N.ptr(out),

@@ -76,7 +76,7 @@ class PatchQuant:
         if calc not in (np.float32, np.float64):
             raise TypeError(f"ivclab_amd: {what} arithmetic in {calc} is not supported")
         src, C, out_shape = _as_blocks(x, table)
-        out = np.empty(out_shape, dtype=np.int32)
+        out = N.empty(out_shape, np.int32)
         nblk = out.size // 192
         if nblk == 0:
             return out

@@ -33,7 +33,7 @@ def rgb2gray(image: np.array):
     if C == 0 or C >= 8:
         raise NotImplementedError("rgb2gray: 1 to 7 channels are supported")
     x = _kernel_input(a, "rgb2gray")
-    out = np.empty(a.shape[:-1] + (1,), np.float32 if x.dtype == np.float32 else np.float64)
+    out = N.empty(a.shape[:-1] + (1,), np.float32 if x.dtype == np.float32 else np.float64)
     npix = x.size // C
     N.check(N.lib().ivc_rgb2gray(N.ptr(x), N.DTYPE_CODE[x.dtype], npix, C, N.ptr(out)), "rgb2gray")
     return out
@@ -45,7 +45,7 @@ def rgb2ycbcr(image: np.array):
     if a.ndim == 0 or a.shape[-1] != 3:
         np.matmul(np.zeros(a.shape[-1:] if a.ndim else (), a.dtype), _M.T)   # NumPy's own error
     x = _kernel_input(a, "rgb2ycbcr")
-    out = np.empty(a.shape, np.float64)
+    out = N.empty(a.shape, np.float64)
     N.check(N.lib().ivc_rgb2ycbcr(N.ptr(x), N.DTYPE_CODE[x.dtype], x.size // 3, N.ptr(out)),
             "rgb2ycbcr")
     return out
@@ -61,7 +61,7 @@ def ycbcr2rgb(image: np.array):
     if a.shape[2] < 3:
         a[:, :, 2]
     x = _kernel_input(a, "ycbcr2rgb")
-    out = np.empty(a.shape[:2] + (3,), np.float32 if x.dtype == np.float32 else np.float64)
+    out = N.empty(a.shape[:2] + (3,), np.float32 if x.dtype == np.float32 else np.float64)
     N.check(N.lib().ivc_ycbcr2rgb(N.ptr(x), N.DTYPE_CODE[x.dtype], a.shape[0] * a.shape[1],
                                   a.shape[2], N.ptr(out)), "ycbcr2rgb")
     return out

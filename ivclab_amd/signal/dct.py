@@ -33,7 +33,7 @@ def dct2d(a, norm="ortho", inverse=False) -> np.ndarray:
     if x.dtype not in N.DTYPE_CODE:
         raise TypeError(f"ivclab_amd: unsupported dtype {x.dtype} for the DCT")
     out_dtype = np.float32 if x.dtype == np.float32 else np.float64
-    out = np.empty(x.shape, dtype=out_dtype)
+    out = N.empty(x.shape, out_dtype)
     nblk = x.size // 64
     if nblk == 0:
         return out

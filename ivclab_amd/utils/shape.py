@@ -48,7 +48,7 @@ class ZigZag:
                              f"not be broadcast to indexing result of shape {(h, w, c, 64)}")
         _check_elem(x, "ZigZag.flatten")
         x = np.ascontiguousarray(x)
-        out = np.empty((h, w, c, 64), dtype=x.dtype)
+        out = N.empty((h, w, c, 64), x.dtype)
         nrow = h * w * c
         if nrow:
             N.check(N.lib().ivc_zigzag(N.ptr(x), nrow, 64, x.dtype.itemsize, 0, N.ptr(out)),
@@ -68,7 +68,7 @@ class ZigZag:
                              f"for axis 3 with size {n}")
         _check_elem(x, "ZigZag.unflatten")
         x = np.ascontiguousarray(x)
-        out = np.empty((h, w, c, 8, 8), dtype=x.dtype)
+        out = N.empty((h, w, c, 8, 8), x.dtype)
         nrow = h * w * c
         if nrow:
             N.check(N.lib().ivc_zigzag(N.ptr(x), nrow, n, x.dtype.itemsize, 1, N.ptr(out)),

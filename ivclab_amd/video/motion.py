@@ -69,7 +69,7 @@ class MotionCompensator:
             raise TypeError(f"ivclab_amd: unsupported dtype {ref.dtype} for motion compensation")
         mvc = np.ascontiguousarray(mv[:h, :w, 0], dtype=np.int64)
         ref = np.ascontiguousarray(ref)
-        out = np.empty_like(ref)
+        out = N.empty_like(ref)
         if out.size:
             N.check(N.lib().ivc_motion_compensate(N.ptr(ref), ref.dtype.itemsize, 1, H, W, C,
                                                   N.ptr(mvc), sr, N.ptr(out)),

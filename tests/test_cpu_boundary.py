@@ -25,7 +25,7 @@ def lib():
 
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "ivc.h")).read()
-    decl = r"^\s*(?:int|int64_t|double|const char\s*\*)\s*(ivc_[a-z0-9_]+)\s*\("
+    decl = r"^\s*(?:int|int64_t|double|void\s*\*|const char\s*\*)\s*(ivc_[a-z0-9_]+)\s*\("
     return sorted(set(re.findall(decl, src, re.M)))
 
 

@@ -377,6 +377,27 @@ def test_intra_encode_4k_full_frame():
     assert_bits(out[0], want, "4K intra")
 
 
+@pytest.mark.parametrize("zz", [False, True])
+@pytest.mark.parametrize("scale", [1.0, 0.013])
+def test_intra_encode_luma_only_vs_oracle(zz, scale):
+    """ivc_intra_encode_luma_dev: plane 0 (the luminance table) of the reference's 3-plane
+    quantisation of a grayscale batch, [F, h, w, 64] int32; ragged groups (w = 33 blocks) and
+    a fine scale (magnitude-checked quotients)."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(int(zz) + 7)
+    F, H, W = 3, 72, 264
+    img = rng.integers(0, 256, (F, H, W), dtype=np.uint8)
+    img[:, :16] = 77
+    table = PatchQuant(scale).get_quantization_table()
+    out = torch.full((F, H // 8, W // 8, 64), -5, dtype=torch.int32, device="cuda")
+    D.intra_encode_luma(torch.from_numpy(img).cuda(), table, out, zigzag=zz)
+    torch.cuda.synchronize()
+    for f in range(F):
+        want = O.intra_encode(img[f][..., None], scale, zigzag=zz)[:, :, 0].reshape(H // 8, W // 8, 64)
+        assert_bits(out[f].cpu().numpy(), want, f"luma-only frame {f}")
+
+
 def test_store_pacing_changes_timing_only():
     """Paced launches (8 4K frames: every wave stores >= 8 slots, so the clock schedule is
     live) give the same bytes as unpaced ones at any rate — far too fast (every slot late),
@@ -484,6 +505,39 @@ def test_store_pace_trace_settle_and_threads():
     want = O.intra_encode(img[0], 1.0).reshape(H // 8, W // 8, 3, 64)
     for oo in [o] + outs:
         assert_bits(oo[0].cpu().numpy(), want, "paced 4K frame 0")
+
+
+def test_pinned_host_pool_and_staging():
+    """ivc_host_alloc blocks back the drop-in classes' large results (ivclab_amd._native.empty):
+    a freed block is reused for the next array of that size, a foreign pointer is refused,
+    and host-buffer calls give identical results from pinned and from pageable buffers, for
+    transfers that take the direct DMA, the pinned ring (several 8 MiB chunks, H2D and D2H)
+    and the small pageable path."""
+    import gc
+    N, L = _native()
+    a = N.empty((1024, 1024), np.float64)
+    p = a.ctypes.data
+    assert not a.flags.owndata and a.flags.writeable
+    del a
+    gc.collect()
+    b = N.empty((1024, 1024), np.float64)
+    assert b.ctypes.data == p
+    assert L.ivc_host_free(None) == 0
+    assert L.ivc_host_free(p + 64) == N.E_ARG
+    rng = np.random.default_rng(3)
+    for nblk in (100, 40_000, 300_000):                  # 0.05, 20 and 150 MB of float64 out
+        src = rng.integers(0, 256, (nblk, 64), dtype=np.uint8)
+        want = O.dct_transform(src.reshape(nblk, 8, 8).astype(np.float64))
+        for out in (np.empty((nblk, 8, 8)), N.empty((nblk, 8, 8), np.float64)):
+            N.check(L.ivc_dct8x8(N.ptr(src), 1, nblk, N.ptr(out), N.F64, 0, 1))
+            assert_bits(out, want, f"dct {nblk} blocks")
+        # float64 input through the ring (H2D chunks), pinned and pageable
+        srcf = src.astype(np.float64)
+        for inp in (srcf, N.empty(srcf.shape, np.float64)):
+            inp[...] = srcf
+            out = N.empty((nblk, 8, 8), np.float64)
+            N.check(L.ivc_dct8x8(N.ptr(inp), N.F64, nblk, N.ptr(out), N.F64, 0, 1))
+            assert_bits(out, want, f"dct f64 in {nblk} blocks")
 
 
 def test_histogram_vs_oracle():
@@ -1163,6 +1217,18 @@ def test_stats_marg_gpu_vs_oracle():
         x = rng.integers(-300 if dt != np.uint8 else 0, 256, (50, 60)).astype(dt)
         for edges in (np.arange(256), np.arange(-20, 41), np.arange(10, 12)):
             assert_bits(stats_marg(x, edges), O.stats_marg(x, edges), f"{dt} {edges[0]}")
+    # 64-bit and unsigned 32-bit data stay on the integer kernels (int64 path) while the edges
+    # lie inside +-2^53: values beyond 2^53 / 2^63, and edges near +-2^52 and past int32
+    big = np.array([0, 5, -7, 1 << 53, (1 << 53) + 1, -(1 << 60), np.iinfo(np.int64).max,
+                    np.iinfo(np.int64).min, (1 << 52) - 1, -(1 << 52), 3_000_000_000], np.int64)
+    for edges in (np.arange(-8, 9), np.arange((1 << 52) - 3, (1 << 52) + 2),
+                  np.arange(-(1 << 52) - 2, -(1 << 52) + 3), np.arange(2_999_999_998, 3_000_000_003)):
+        assert_bits(stats_marg(big, edges), O.stats_marg(big, edges), f"int64 {edges[0]}")
+    u = np.array([0, 1, 7, 1 << 63, (1 << 64) - 1, 4_000_000_000], np.uint64)
+    for edges in (np.arange(0, 9), np.arange(3_999_999_998, 4_000_000_002)):
+        assert_bits(stats_marg(u, edges), O.stats_marg(u, edges), f"uint64 {edges[0]}")
+        u32 = np.array([0, 1, 7, 3_999_999_999, 4_000_000_000, (1 << 32) - 1], np.uint32)
+        assert_bits(stats_marg(u32, edges), O.stats_marg(u32, edges), f"uint32 {edges[0]}")
 
 
 STATS = ["u8_full", "i16_window", "i64_unit", "f64_linspace", "f32_nonuniform", "f64_intbins",
