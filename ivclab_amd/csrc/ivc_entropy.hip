@@ -22,10 +22,14 @@ namespace ivc {
 
 // ---------------------------------------------------------------- generic tile scan ---
 // Exclusive scan of gen(i), i in [0, n), with an associative Op over T; sink(i, excl, v)
-// receives every element's exclusive prefix.  Three kernels: tile aggregates, a one-
-// workgroup scan of the aggregates, and the tile-local scan.  Each thread owns SCAN_I
-// consecutive elements.
+// receives every element's exclusive prefix.  Three kernels: tile aggregates, an exclusive
+// scan of the aggregates (one workgroup when they fit one tile, else the same scan applied to
+// them, recursively), and the tile-local scan.  Each thread owns SCAN_I consecutive elements;
+// the tile kernels loop over tiles (grid capped at SCAN_GRID workgroups).  `skip` (device
+// int, may be null): when nonzero at launch every kernel returns at once (a decode whose fast
+// path succeeded skips the general one without a host round trip).
 constexpr int SCAN_T = 256, SCAN_I = 8, SCAN_TILE = SCAN_T * SCAN_I;
+constexpr int64_t SCAN_GRID = 256 * 8;
 
 // (EOB value slots before, segment-contains-EOB flag, length since the last EOB): the
 // decoder's scan state (declared here so the shuffle overloads precede the templates)
@@ -70,21 +74,29 @@ __device__ T wg_excl_scan(T v, Op op, T* lds4, T& total) {
 }
 
 template <typename T, typename Op, typename Gen>
-__global__ __launch_bounds__(SCAN_T) void scan_tile_aggregate(int64_t n, Gen gen, Op op, T* agg) {
+__global__ __launch_bounds__(SCAN_T) void scan_tile_aggregate(int64_t n, Gen gen, Op op, T* agg,
+                                                              const int* skip) {
+  if (skip && *skip) return;
   __shared__ T lds4[4];
-  const int64_t i0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
-  T v = Op::identity();
+  const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t i0 = t * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+    T v = Op::identity();
 #pragma unroll
-  for (int k = 0; k < SCAN_I; ++k)
-    if (i0 + k < n) v = op(v, gen(i0 + k));
-  T total;
-  (void)wg_excl_scan(v, op, lds4, total);
-  if (threadIdx.x == 0) agg[blockIdx.x] = total;
+    for (int k = 0; k < SCAN_I; ++k)
+      if (i0 + k < n) v = op(v, gen(i0 + k));
+    T total;
+    (void)wg_excl_scan(v, op, lds4, total);
+    if (threadIdx.x == 0) agg[t] = total;
+  }
 }
 
-// exclusive scan of the tile aggregates in place (one workgroup); agg[ntiles] = total
+// exclusive scan of at most SCAN_TILE tile aggregates in place (one workgroup); agg[ntiles] =
+// total
 template <typename T, typename Op>
-__global__ __launch_bounds__(SCAN_T) void scan_aggregates(T* agg, int64_t ntiles, Op op) {
+__global__ __launch_bounds__(SCAN_T) void scan_aggregates(T* agg, int64_t ntiles, Op op,
+                                                          const int* skip) {
+  if (skip && *skip) return;
   __shared__ T lds4[4];
   T carry = Op::identity();
   for (int64_t base = 0; base < ntiles; base += SCAN_T) {
@@ -100,37 +112,73 @@ __global__ __launch_bounds__(SCAN_T) void scan_aggregates(T* agg, int64_t ntiles
 
 template <typename T, typename Op, typename Gen, typename Sink>
 __global__ __launch_bounds__(SCAN_T) void scan_tile_apply(int64_t n, Gen gen, Op op,
-                                                          const T* agg, Sink sink) {
+                                                          const T* agg, Sink sink,
+                                                          const int* skip) {
+  if (skip && *skip) return;
   __shared__ T lds4[4];
-  const int64_t i0 = (int64_t)blockIdx.x * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
-  T vals[SCAN_I];
-  T v = Op::identity();
+  const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t i0 = t * SCAN_TILE + (int64_t)threadIdx.x * SCAN_I;
+    T vals[SCAN_I];
+    T v = Op::identity();
 #pragma unroll
-  for (int k = 0; k < SCAN_I; ++k) {
-    vals[k] = i0 + k < n ? gen(i0 + k) : Op::identity();
-    v = op(v, vals[k]);
-  }
-  T total;
-  T run = op(agg[blockIdx.x], wg_excl_scan(v, op, lds4, total));
+    for (int k = 0; k < SCAN_I; ++k) {
+      vals[k] = i0 + k < n ? gen(i0 + k) : Op::identity();
+      v = op(v, vals[k]);
+    }
+    T total;
+    T run = op(agg[t], wg_excl_scan(v, op, lds4, total));
 #pragma unroll
-  for (int k = 0; k < SCAN_I; ++k) {
-    if (i0 + k < n) sink(i0 + k, run, vals[k]);
-    run = op(run, vals[k]);
+    for (int k = 0; k < SCAN_I; ++k) {
+      if (i0 + k < n) sink(i0 + k, run, vals[k]);
+      run = op(run, vals[k]);
+    }
   }
 }
 
-// agg: device scratch of >= ntiles + 1 elements
+// the recursive level: the aggregates themselves, scanned in place (each element is read and
+// rewritten by the same thread), a[n] = total
+template <typename T>
+struct AggGen {
+  const T* a;
+  __device__ T operator()(int64_t i) const { return a[i]; }
+};
+template <typename T, typename Op>
+struct AggSink {
+  T* a;
+  int64_t n;
+  __device__ void operator()(int64_t i, const T& excl, const T& v) const {
+    a[i] = excl;
+    if (i == n - 1) a[n] = Op{}(excl, v);
+  }
+};
+
+// elements of T the scan of n values needs as scratch: every level's aggregates + total
+static int64_t scan_levels_elems(int64_t n) {
+  const int64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
+  return nt + 1 + (nt > SCAN_TILE ? scan_levels_elems(nt) : 0);
+}
+
+// agg: device scratch of >= scan_levels_elems(n) elements
 template <typename T, typename Op, typename Gen, typename Sink>
-static hipError_t device_scan(int64_t n, Gen gen, Op op, Sink sink, T* agg, hipStream_t s) {
+static hipError_t device_scan(int64_t n, Gen gen, Op op, Sink sink, T* agg, hipStream_t s,
+                              const int* skip = nullptr) {
   if (n <= 0) return hipSuccess;
   const int64_t ntiles = (n + SCAN_TILE - 1) / SCAN_TILE;
-  scan_tile_aggregate<T, Op, Gen><<<(unsigned)ntiles, SCAN_T, 0, s>>>(n, gen, op, agg);
-  scan_aggregates<T, Op><<<1, SCAN_T, 0, s>>>(agg, ntiles, op);
-  scan_tile_apply<T, Op, Gen, Sink><<<(unsigned)ntiles, SCAN_T, 0, s>>>(n, gen, op, agg, sink);
+  const unsigned grid = (unsigned)(ntiles < SCAN_GRID ? ntiles : SCAN_GRID);
+  scan_tile_aggregate<T, Op, Gen><<<grid, SCAN_T, 0, s>>>(n, gen, op, agg, skip);
+  if (ntiles <= SCAN_TILE) {
+    scan_aggregates<T, Op><<<1, SCAN_T, 0, s>>>(agg, ntiles, op, skip);
+  } else {
+    const hipError_t e = device_scan<T>(ntiles, AggGen<T>{agg}, op, AggSink<T, Op>{agg, ntiles},
+                                        agg + ntiles + 1, s, skip);
+    if (e != hipSuccess) return e;
+  }
+  scan_tile_apply<T, Op, Gen, Sink><<<grid, SCAN_T, 0, s>>>(n, gen, op, agg, sink, skip);
   return hipGetLastError();
 }
 
-int64_t scan_scratch_elems(int64_t n) { return (n + SCAN_TILE - 1) / SCAN_TILE + 1; }
+int64_t scan_scratch_elems(int64_t n) { return scan_levels_elems(n); }
 
 struct SumI64 {
   __device__ int64_t operator()(int64_t a, int64_t b) const { return a + b; }
@@ -604,9 +652,9 @@ struct ZrSink {
 
 // err[0] = code (0 ok, 1 block size exceeded, 2 unexpected end, 3 ended right after a zero
 // symbol, 4 too few blocks), err[1], err[2] = message arguments
-__global__ void zr_decode_verdict(const int32_t* s, const uint8_t* is_rl, int64_t n,
-                                  int64_t expected, int32_t eob, const ZrState* total,
-                                  const unsigned long long* first_overflow, int64_t* err) {
+__device__ void zr_decode_verdict_body(const int32_t* s, const uint8_t* is_rl, int64_t n,
+                                       int64_t expected, int32_t eob, const ZrState* total,
+                                       const unsigned long long* first_overflow, int64_t* err) {
   const unsigned long long ov = *first_overflow;
   int64_t code = 0, a0 = 0, a1 = 0;
   const int64_t got = n > 0 ? total->blocks : 0;
@@ -649,35 +697,264 @@ struct BothSinks {
   }
 };
 
-int64_t zr_decode_scratch_bytes(int64_t n) {
-  // is_rl (n bytes, 16-aligned) + int64 aggregates + ZrState aggregates + total + overflow
+// ---- fast decode of well-formed streams ----------------------------------------------
+// In a stream with no two adjacent zero symbols and no run length <= 0 — every stream the
+// encoder emits — slot i is a run-length slot iff symbol i - 1 is 0 (a zero can then only be
+// a value slot: a zero run-length slot would follow a zero value slot), so typing is local
+// and the EOB value slots (the block ends) are symbols equal to eob after a nonzero.  Two
+// passes: (1) per tile of ZF_TILE symbols, count the EOB slots and test the two conditions
+// (16-byte loads, one read of the stream); an int64 scan of the tile counts gives each tile's
+// first block; (2) per tile, the blocks whose EOB lies in it (the first one starts in the
+// previous tile: a halo of ZF_HALO symbols, longer than any block) are expanded one per wave
+// iteration — lane j takes symbol j of the block, its coefficient count (1 for a nonzero
+// value, the run length for a zero, 0 for a run-length slot) is prefix-summed across the
+// wave, and the nonzero values land in a zeroed 64-entry row written with one coalesced
+// store.  Any violation (a block longer than B coefficients or than the halo, fewer blocks
+// than expected, adjacent zeros, a non-positive run, eob = 0) sets `fail`, and the general
+// decoder above runs instead (its kernels read the verdict on the device: no host round
+// trip), so errors and their messages are the general decoder's.
+constexpr int ZF_TILE = 4096, ZF_HALO = 128;
+
+__global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict__ s, int64_t n,
+                                                       int32_t eob, int32_t* __restrict__ tile_eobs,
+                                                       int* fail) {
+  __shared__ int red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t ntiles = (n + ZF_TILE - 1) / ZF_TILE;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    int cnt = 0;
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < ZF_TILE / 1024; ++k) {
+      const int64_t i = t * ZF_TILE + (int64_t)(k * 256 + tid) * 4;
+      int v[4];
+      if (i + 3 < n) {
+        typedef int i32x4 __attribute__((ext_vector_type(4)));
+        const i32x4 q = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(s + i));
+        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = i + e < n ? s[i + e] : 1;
+      }
+      int pv = i > 0 && i < n ? s[i - 1] : 1;       // the stream's first slot is a value slot
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (i + e < n) {
+          cnt += (v[e] == eob && pv != 0) ? 1 : 0;
+          bad |= pv == 0 && v[e] <= 0;
+        }
+        pv = v[e];
+      }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
+    if (__ballot(bad) && lane == 0) atomicOr(fail, 1);
+    if (lane == 0) red[wave] = cnt;
+    __syncthreads();
+    if (tid == 0) tile_eobs[t] = red[0] + red[1] + red[2] + red[3];
+    __syncthreads();
+  }
+}
+
+// inclusive prefix sum over the wave by DPP (no LDS round trips): Hillis-Steele inside each
+// row of 16 lanes (row_shr 1, 2, 4, 8), then row_bcast:15 carries row 0 into row 1 and row 2
+// into row 3, row_bcast:31 carries rows 0-1 into rows 2-3 (CDNA keeps the GFX9 broadcasts)
+__device__ __forceinline__ int zf_wave_incl_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return v;
+}
+
+__global__ __launch_bounds__(256) void zf_expand_kernel(const int32_t* __restrict__ s, int64_t n,
+                                                        int32_t eob, int B,
+                                                        const int64_t* __restrict__ tile_first,
+                                                        int64_t expected, int32_t* __restrict__ out,
+                                                        int* fail) {
+  __shared__ int32_t sh[ZF_HALO + ZF_TILE + 4];
+  __shared__ int32_t epos[ZF_TILE];         // EOB slots of the tile, relative to the halo start
+  __shared__ int32_t rows[4][64];
+  __shared__ int cnt_w[4], last_halo;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t ntiles = (n + ZF_TILE - 1) / ZF_TILE;
+  constexpr int PER = ZF_TILE / 256;        // tile symbols per thread (EOB compaction)
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t T0 = t * ZF_TILE, T1 = T0 + ZF_TILE < n ? T0 + ZF_TILE : n;
+    const int64_t h0 = T0 - ZF_HALO > 0 ? T0 - ZF_HALO : 0;
+    const int len = (int)(T1 - h0);          // symbols staged (halo + tile)
+    const int hl = (int)(T0 - h0);           // halo length
+    for (int j = tid; j < len; j += 256) sh[j] = s[h0 + j];
+    if (tid == 0) last_halo = T0 == 0 ? -1 : -2;
+    __syncthreads();
+    auto is_eob = [&](int j) {               // j relative to h0, symbol h0 + j
+      return sh[j] == eob && (h0 + j == 0 || sh[j - 1] != 0);
+    };
+    // the last EOB of the halo: where the tile's first block starts
+    if (tid < hl && is_eob(tid)) atomicMax(&last_halo, tid);
+    // EOB slots of the tile, compacted in stream order (thread = PER consecutive symbols)
+    const int j0 = hl + tid * PER;
+    int c = 0;
+#pragma unroll
+    for (int e = 0; e < PER; ++e) c += (j0 + e < len && is_eob(j0 + e)) ? 1 : 0;
+    const int incl = zf_wave_incl_sum(c);
+    if (lane == 63) cnt_w[wave] = incl;
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wave; ++w) before += cnt_w[w];
+    const int m = cnt_w[0] + cnt_w[1] + cnt_w[2] + cnt_w[3];
+    int o = before + incl - c;
+#pragma unroll
+    for (int e = 0; e < PER; ++e)
+      if (j0 + e < len && is_eob(j0 + e)) epos[o++] = j0 + e;
+    __syncthreads();
+    if (m > 0 && last_halo == -2 && tid == 0) atomicOr(fail, 1);   // a block longer than the halo
+    const int64_t first = tile_first[t];
+    for (int k = wave; k < m; k += 4) {
+      const int64_t blk = first + k;
+      if (blk >= expected) break;
+      const int st = (k == 0 ? last_halo : epos[k - 1]) + 1, en = epos[k];
+      const int bl = en - st;                // symbols before the EOB
+      int32_t* row = rows[wave];
+      row[lane] = 0;
+      if (bl > 128 || st < 0) {              // only in a malformed stream
+        if (lane == 0) atomicOr(fail, 1);
+        continue;
+      }
+      int carry = 0;
+      bool over = false;
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int j = half * 64 + lane;
+        const bool valid = j < bl;
+        const int cur = valid ? sh[st + j] : 1;
+        const int pv = j == 0 ? 1 : sh[st + j - 1];
+        const bool rl = valid && pv == 0;
+        const int cc = !valid || rl ? 0 : (cur == 0 ? sh[st + j + 1] : 1);
+        const int inc = zf_wave_incl_sum(cc);
+        const int pos = carry + inc - cc;
+        if (valid && !rl && cur != 0 && pos < B) row[pos] = cur;
+        carry += __builtin_amdgcn_readlane(inc, 63);
+        if (bl <= 64) break;
+      }
+      over = carry > B;
+      __builtin_amdgcn_wave_barrier();
+      if (over) {
+        if (lane == 0) atomicOr(fail, 1);
+      } else if (lane < B) {
+        out[blk * B + lane] = row[lane];
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+  }
+}
+
+// ok = the fast decode stands (no violation, enough blocks): err = 0; else the general
+// decoder runs (its kernels see ok == 0)
+__global__ void zf_finish(const int* fail, const int64_t* total_eobs, int64_t expected, int* ok,
+                          int64_t* err) {
+  const bool good = *fail == 0 && *total_eobs >= expected;
+  *ok = good ? 1 : 0;
+  if (good) {
+    err[0] = 0;
+    err[1] = 0;
+    err[2] = 0;
+  }
+}
+
+__global__ void zr_zero_fill(int32_t* out, int64_t count, const int* skip) {
+  if (skip && *skip) return;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < count; i += (int64_t)gridDim.x * 256)
+    out[i] = 0;
+}
+
+__global__ void zr_decode_verdict_gated(const int32_t* s, const uint8_t* is_rl, int64_t n,
+                                        int64_t expected, int32_t eob, const ZrState* total,
+                                        const unsigned long long* first_overflow, int64_t* err,
+                                        const int* skip) {
+  if (skip && *skip) return;
+  zr_decode_verdict_body(s, is_rl, n, expected, eob, total, first_overflow, err);
+}
+
+namespace {
+struct ZrDecScratch {
+  uint8_t* is_rl;
+  int64_t* agg;
+  ZrState* zagg;
+  ZrState* total;
+  unsigned long long* ovf;
+  int32_t* tile_eobs;
+  int64_t* tile_first;      // ntf + 1
+  int64_t* fagg;
+  int* flags;               // [0] fail, [1] ok
+};
+int64_t align16(int64_t b) { return (b + 15) / 16 * 16; }
+ZrDecScratch zr_dec_scratch(void* scratch, int64_t n, int64_t* bytes) {
   const int64_t nt = scan_scratch_elems(n);
-  return ((n + 15) / 16) * 16 + nt * 8 + nt * (int64_t)sizeof(ZrState) + 64;
+  const int64_t ntf = (n + ZF_TILE - 1) / ZF_TILE;
+  uint8_t* b = (uint8_t*)scratch;
+  ZrDecScratch z;
+  int64_t o = 0;
+  z.is_rl = b + o; o += align16(n);
+  z.agg = (int64_t*)(b + o); o += align16(nt * 8);
+  z.zagg = (ZrState*)(b + o); o += align16(nt * (int64_t)sizeof(ZrState));
+  z.total = (ZrState*)(b + o); o += align16(sizeof(ZrState));
+  z.ovf = (unsigned long long*)(b + o); o += 16;
+  z.tile_eobs = (int32_t*)(b + o); o += align16(ntf * 4);
+  z.tile_first = (int64_t*)(b + o); o += align16((ntf + 1) * 8);
+  z.fagg = (int64_t*)(b + o); o += align16(scan_scratch_elems(ntf) * 8);
+  z.flags = (int*)(b + o); o += 16;
+  if (bytes) *bytes = o;
+  return z;
+}
+}  // namespace
+
+int64_t zr_decode_scratch_bytes(int64_t n) {
+  int64_t bytes = 0;
+  (void)zr_dec_scratch(nullptr, n, &bytes);
+  return bytes;
 }
 
 hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected, int B,
                                  int32_t eob, int32_t* out, void* scratch, int64_t* err,
                                  hipStream_t s) {
-  const int64_t nt = scan_scratch_elems(n);
-  uint8_t* base = (uint8_t*)scratch;
-  uint8_t* is_rl = base;
-  int64_t* agg = (int64_t*)(base + ((n + 15) / 16) * 16);
-  ZrState* zagg = (ZrState*)(agg + nt);
-  ZrState* total = zagg + nt;
-  unsigned long long* ovf = (unsigned long long*)(total + 1);
+  const ZrDecScratch z = zr_dec_scratch(scratch, n, nullptr);
   hipError_t e;
-  if ((e = hipMemsetAsync(out, 0, (size_t)expected * B * sizeof(int32_t), s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(ovf, 0xff, sizeof(unsigned long long), s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(total, 0, sizeof(ZrState), s)) != hipSuccess) return e;
-  if (n > 0) {
-    e = device_scan<int64_t>(n, NzPosGen{sym}, MaxI64{}, RlTypeSink{is_rl}, agg, s);
+  const int* skip = nullptr;
+  if (n > 0 && expected > 0 && B >= 1 && B <= 64 && eob != 0 && ((uintptr_t)sym & 15) == 0) {
+    const int64_t ntf = (n + ZF_TILE - 1) / ZF_TILE;
+    const unsigned grid = (unsigned)(ntf < 256 * 8 ? ntf : 256 * 8);
+    if ((e = hipMemsetAsync(z.flags, 0, 16, s)) != hipSuccess) return e;
+    zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags);
+    e = device_scan<int64_t>(ntf, CountGen{z.tile_eobs}, SumI64{}, OffsetSink{z.tile_first, ntf},
+                             z.fagg, s);
     if (e != hipSuccess) return e;
-    ZrSink place{sym, is_rl, n, expected, B, eob, out, ovf};
-    e = device_scan<ZrState>(n, ZrGen{sym, is_rl, n, eob}, ZrOp{},
-                             BothSinks<ZrSink, ZrTotalSink>{place, ZrTotalSink{total, n}}, zagg, s);
+    zf_expand_kernel<<<grid, 256, 0, s>>>(sym, n, eob, B, z.tile_first, expected, out, z.flags);
+    zf_finish<<<1, 1, 0, s>>>(z.flags, z.tile_first + ntf, expected, z.flags + 1, err);
+    skip = z.flags + 1;
+  }
+  // the general decoder (every stream; skipped on the device when the fast one stood)
+  if ((e = hipMemsetAsync(z.ovf, 0xff, sizeof(unsigned long long), s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(z.total, 0, sizeof(ZrState), s)) != hipSuccess) return e;
+  const int64_t nz = expected * B;
+  if (nz > 0) {
+    const int64_t g = (nz + 255) / 256;
+    zr_zero_fill<<<(unsigned)(g < 256 * 16 ? g : 256 * 16), 256, 0, s>>>(out, nz, skip);
+  }
+  if (n > 0) {
+    e = device_scan<int64_t>(n, NzPosGen{sym}, MaxI64{}, RlTypeSink{z.is_rl}, z.agg, s, skip);
+    if (e != hipSuccess) return e;
+    ZrSink place{sym, z.is_rl, n, expected, B, eob, out, z.ovf};
+    e = device_scan<ZrState>(n, ZrGen{sym, z.is_rl, n, eob}, ZrOp{},
+                             BothSinks<ZrSink, ZrTotalSink>{place, ZrTotalSink{z.total, n}}, z.zagg,
+                             s, skip);
     if (e != hipSuccess) return e;
   }
-  zr_decode_verdict<<<1, 1, 0, s>>>(sym, is_rl, n, expected, eob, total, ovf, err);
+  zr_decode_verdict_gated<<<1, 1, 0, s>>>(sym, z.is_rl, n, expected, eob, z.total, z.ovf, err, skip);
   return hipGetLastError();
 }
 

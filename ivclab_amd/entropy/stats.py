@@ -13,6 +13,32 @@ def huffman_bounds(sym_min: int, sym_max: int, safety_margin: int = 20):
     return int(sym_min) - safety_margin, int(sym_max) + safety_margin + 1
 
 
+def bounds_from_histogram(hist, lo):
+    """(min, max) of the symbols a guarded histogram counted — hist[0] = values below lo,
+    hist[1 + k] = value lo + k, hist[-1] = values past the range — or None when any symbol
+    fell outside the range (the caller then takes the exact min/max path)."""
+    h = np.asarray(hist)
+    if h[0] or h[-1]:
+        return None
+    nz = np.flatnonzero(h[1:-1])
+    if nz.size == 0:
+        return None
+    return lo + int(nz[0]), lo + int(nz[-1])
+
+
+def counts_over(hist, lo, b0, b1):
+    """np.histogram counts of the guarded histogram's symbols over the unit edges
+    arange(b0, b1) (last bin closed), given that every symbol lies in [lo, lo + nbins)."""
+    h = np.asarray(hist)[1:-1]
+    v = np.arange(b0, b1 - 1)
+    k = v - lo
+    out = np.where((k >= 0) & (k < h.size), h[np.clip(k, 0, h.size - 1)], 0).astype(np.int64)
+    last = b1 - 1 - lo                          # the closed last bin also holds value b1 - 1
+    if out.size and 0 <= last < h.size:
+        out[-1] += h[last]
+    return out
+
+
 def stats_marg_from_counts(counts, total=None):
     """stats_marg (entropy.py:6-29) given np.histogram's counts: counts / number of
     samples (float64)."""

@@ -745,6 +745,60 @@ def test_zerorun_decode_errors_golden(golden, case):
         assert_bits(ZeroRunCoder().decode(sym, shape), z[f"err_{case}_out"], case)
 
 
+def test_zerorun_decode_fast_path_boundaries():
+    """The fast decoder (ivc_entropy.hip zf_*: local slot typing, 4096-symbol tiles, a
+    128-symbol halo) against the oracle on streams built to stress it: the longest blocks
+    (97 symbols: alternating value / zero-run, crossing tile boundaries), all-EOB stretches
+    longer than the halo, coefficient values equal to the EOB symbol and to the run lengths,
+    and streams it must hand to the general decoder (a zero run-length after a zero value,
+    a negative run, an overflowing block, trailing garbage after the expected blocks, too few
+    blocks, a stream ending after a zero) — results and errors identical either way."""
+    from ivclab_amd.entropy import ZeroRunCoder
+    rng = np.random.default_rng(97)
+    Z = ZeroRunCoder()
+    nb = 3000
+    x = np.zeros((nb, 64), np.int32)
+    kinds = rng.integers(0, 5, nb)
+    for i, k in enumerate(kinds):
+        if k == 0:                                         # longest: v 0 run, repeated
+            x[i, 0::2] = rng.integers(1, 9, 32) * rng.choice([-1, 1], 32)
+        elif k == 1:
+            pass                                           # all-zero: EOB only
+        elif k == 2:
+            x[i] = rng.integers(-3, 4, 64)
+        elif k == 3:
+            x[i, rng.integers(0, 64, 3)] = 4000            # the EOB value as a coefficient
+        else:
+            x[i, :8] = rng.integers(1, 64, 8)              # values equal to run lengths
+    x[1000:1400] = 0                                       # 400 EOBs in a row (> halo)
+    sym = O.zerorun_encode_fast(x)
+    shape = (nb // 30, 30, 1)
+    assert sym.size > 3 * 4096
+    # (the EOB symbol as a coefficient decodes as an EOB in the reference: the stream is then
+    # parsed as the reference parses it, whatever that yields)
+    bad = {
+        "clean": sym,
+        "clean_no_eob_values": O.zerorun_encode_fast(np.where(x == 4000, 4001, x)),
+        "zero_run_zero": np.concatenate([sym[:50], [0, 0, 5], sym[50:]]),
+        "negative_run": np.concatenate([sym[:50], [0, -2], sym[50:]]),
+        "overflow": np.concatenate([[0, 63, 7, 7], sym]),
+        "trailing_garbage": np.concatenate([sym, [0, 0, 0, -5, 4000]]),
+        "too_few": sym[: np.flatnonzero(sym == 4000)[nb // 2]],
+        "ends_after_zero": np.concatenate([sym[: np.flatnonzero(sym == 4000)[10] + 1], [5, 0]]),
+    }
+    for name, s in bad.items():
+        s = np.ascontiguousarray(s, np.int32)
+        try:
+            want = O.zerorun_decode(list(s), shape)
+        except Exception as e:  # noqa: BLE001
+            with pytest.raises(type(e)) as got:
+                Z.decode(s, shape)
+            if not isinstance(e, IndexError):
+                assert str(got.value) == str(e), name
+            continue
+        assert_bits(Z.decode(s, shape), want, name)
+
+
 @pytest.mark.parametrize("bs,p", [(64, 64), (16, 16), (10, 64), (0, 8), (64, 80)])
 def test_zerorun_random_vs_oracle(bs, p):
     """Large random sparse streams (mixed densities, all-zero / full / alternating blocks)
