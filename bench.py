@@ -63,6 +63,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 #   v_dot4_u32_u8 issues at half rate (tools/ubench/valu_rates.hip): 39.3 T lane-instr/s
 #   FP64 add/mul (no FMA: NumPy rounds every product): half the FP32 vector rate, 39.3 T op/s
 DOT4_PEAK_T = 256 * 4 * 64 * 2.4e9 / 4 / 1e12
+# dense i8 MFMA: twice the bf16 rate (MI355X_MICROARCH.md: ~2.5 PF bf16 dense)
+MFMA_I8_PEAK_T = 5000.0
 F64_PEAK_T = 78.6 / 2
 HIST_LO, HIST_BINS = -4096, 8192
 PACE_MARGIN = 0.02             # settle the store pace this far below its lowest failed rate
@@ -713,27 +715,39 @@ def leg_inter(args, dist, rank, world, dev, table, result, verify):
         D.inter_encode(seq, sr, table, mv, q, zigzag=args.zigzag)
 
     iwall, ims = timed(dist, istep, args.inter_steps, 1)
-    # the motion search alone (S2 pre-pass + dot4 search kernels, chunked as inside
-    # inter_encode), timed with events on its stream
+    # the motion search alone (the matrix-core search, or the S2 pre-pass + dot4 search kernels
+    # chunked as inside inter_encode when IVC_ME_MFMA=0), timed with events on its stream
+    from ivclab_amd import _native as N
+    mfma = bool(N.lib().ivc_me_mfma_enabled())
     mv2 = torch.empty_like(mv)
     _, me_ms = timed(None, lambda: D.motion_estimate(seq[:-1], seq[1:], sr, mv2, exact_u8=True),
                      args.inter_steps, 1)
     ipx = (Fi - 1) * Hi * Wi
     cand = valid_candidates(Hi, Wi, sr) * (Fi - 1)
     dot4 = cand * 16                        # 64 px of c*r per candidate = 16 v_dot4 lane-ops
+    macs = cand * 64                        # useful multiply-adds (window x block) per search
     result["inter"] = {
         "metric": "Mpixels/s: 1080p +-16 full-search ME + MC + residual DCT+quant",
         "value": round(world * ipx * args.inter_steps / iwall / 1e6, 1), "unit": "Mpixels/s",
         "ms_per_step": round(iwall / args.inter_steps * 1e3, 3),
         "config": {"workload": f"cfg4: {Fi} frames 1920x1080 u8 luma per GPU, sr={sr}, "
                                "ME against the previous source frame (open loop)"},
-        "roofline": {"bound": "valu (v_dot4_u32_u8)", "kernel": "me_s2_kernel<true> + me_tile16_kernel",
+        "roofline": {"bound": "valu (per-output key selection)" if mfma else "valu (v_dot4_u32_u8)",
+                     "kernel": "me_mfma16_kernel" if mfma else "me_s2_kernel<true> + me_tile16_kernel",
                      "kernel_ms": round(me_ms, 4),
                      "achieved": round(dot4 / (me_ms * 1e-3) / 1e12, 2), "peak": round(DOT4_PEAK_T, 2),
                      "unit": "T dot4 lane-ops/s", "frac": round(dot4 / (me_ms * 1e-3) / 1e12 / DOT4_PEAK_T, 4),
                      "useful_dot4_per_launch": dot4,
-                     "note": "useful work = valid candidates x 64 px / 4 (SSD = sum c^2 + S2 - 2X; "
-                             "X by v_dot4_u32_u8, half-rate issue); S2 pre-pass time included"},
+                     "mfma_i8": {"useful_TOPs": round(2 * macs / (me_ms * 1e-3) / 1e12, 1),
+                                 "peak_TOPs": MFMA_I8_PEAK_T,
+                                 "frac": round(2 * macs / (me_ms * 1e-3) / 1e12 / MFMA_I8_PEAK_T, 4)},
+                     "note": ("useful work = valid candidates x 64 px (SSD = sum c^2 + S2 - 2X); frac is "
+                              "the dot4-equivalent rate (candidates x 16 dot4 lane-ops against the "
+                              "half-rate dot4 VALU peak) so both search kernels share one scale; "
+                              + ("the matrix-core kernel computes 16 blocks x 16 window positions per "
+                                 "MFMA (20.6% of its outputs are candidates) and is bound by the VALU "
+                                 "selection of those outputs, not by the MFMA pipe (mfma_i8.frac)"
+                                 if mfma else "S2 pre-pass time included"))},
     }
     if verify is not None:
         torch.cuda.synchronize()

@@ -52,6 +52,9 @@ enum ivc_status {
 /* ---------------------------------------------------------------- runtime ---------- */
 const char* ivc_last_error(void);
 int ivc_version(void);
+/* 1 if the exact-u8 +-16 motion search runs on the matrix cores (me_mfma16_kernel; environment
+   IVC_ME_MFMA=0 selects the dot4 search me_tile16_kernel), 0 otherwise */
+int ivc_me_mfma_enabled(void);
 int ivc_device_count(void);
 int ivc_set_device(int device);
 /* 1 if the loaded code object matches the current device (gfx950), 0 otherwise */

@@ -37,6 +37,7 @@ _P, _I, _L = _ct.c_void_p, _ct.c_int, _ct.c_int64
 _SIGS = {
     "ivc_last_error": ([], _ct.c_char_p),
     "ivc_version": ([], _I),
+    "ivc_me_mfma_enabled": ([], _I),
     "ivc_device_count": ([], _I),
     "ivc_set_device": ([_I], _I),
     "ivc_device_ok": ([], _I),

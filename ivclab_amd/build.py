@@ -14,8 +14,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libivc.so")
-SOURCES = ["ivc_kernels.hip", "ivc_motion.hip", "ivc_entropy.hip", "ivc_decode.hip", "ivc_color.hip",
-           "ivc_huffman.hip", "ivc_capi.hip"]
+SOURCES = ["ivc_kernels.hip", "ivc_motion.hip", "ivc_me_mfma.hip", "ivc_entropy.hip", "ivc_decode.hip",
+           "ivc_color.hip", "ivc_huffman.hip", "ivc_capi.hip"]
 HEADERS = ["ivc_math.h", "ivc_internal.h", os.path.join("..", "..", "include", "ivc.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]

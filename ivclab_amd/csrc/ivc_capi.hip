@@ -331,6 +331,7 @@ extern "C" {
 
 const char* ivc_last_error(void) { return g_err.c_str(); }
 int ivc_version(void) { return 10000; }
+int ivc_me_mfma_enabled(void) { return me_use_mfma() ? 1 : 0; }
 
 int ivc_device_count(void) {
   int n = 0;

@@ -774,7 +774,7 @@ __global__ __launch_bounds__(256) void zf_expand_kernel(const int32_t* __restric
                                                         const int64_t* __restrict__ tile_first,
                                                         int64_t expected, int32_t* __restrict__ out,
                                                         int* fail) {
-  __shared__ int32_t sh[ZF_HALO + ZF_TILE + 4];
+  __shared__ __attribute__((aligned(16))) int32_t sh[ZF_HALO + ZF_TILE + 4];
   __shared__ int32_t epos[ZF_TILE];         // EOB slots of the tile, relative to the halo start
   __shared__ int32_t rows[4][64];
   __shared__ int cnt_w[4], last_halo;
@@ -786,7 +786,29 @@ __global__ __launch_bounds__(256) void zf_expand_kernel(const int32_t* __restric
     const int64_t h0 = T0 - ZF_HALO > 0 ? T0 - ZF_HALO : 0;
     const int len = (int)(T1 - h0);          // symbols staged (halo + tile)
     const int hl = (int)(T0 - h0);           // halo length
-    for (int j = tid; j < len; j += 256) sh[j] = s[h0 + j];
+    {
+      // 16-byte loads, all in flight before the first LDS write (h0 is a multiple of 4 and
+      // the stream 16-byte aligned; the quad past the stream's end goes element by element)
+      typedef int i32x4 __attribute__((ext_vector_type(4)));
+      constexpr int NQ = (ZF_HALO + ZF_TILE) / 4 / 256 + 1;
+      i32x4 q[NQ];
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) {
+        const int j = 4 * (tid + 256 * k);
+        if (j + 3 < len) {
+          q[k] = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(s + h0 + j));
+        } else {
+          q[k] = i32x4{0, 0, 0, 0};
+          for (int e = 0; e < 4; ++e)
+            if (j + e < len) q[k][e] = s[h0 + j + e];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NQ; ++k) {
+        const int j = 4 * (tid + 256 * k);
+        if (j < len) *reinterpret_cast<i32x4*>(sh + j) = q[k];
+      }
+    }
     if (tid == 0) last_halo = T0 == 0 ? -1 : -2;
     __syncthreads();
     auto is_eob = [&](int j) {               // j relative to h0, symbol h0 + j

@@ -14,6 +14,8 @@
 // and combined with that key.
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "ivc_internal.h"
 
 namespace ivc {
@@ -473,6 +475,9 @@ static unsigned me_fast_grid(const void* kernel, int64_t wgs) {
 #endif
 #ifndef IVC_ME_ABL
 #define IVC_ME_ABL 0                       // diagnostic builds: bit mask of skipped phases
+#endif
+#ifndef IVC_ME_MFMA_DEFAULT
+#define IVC_ME_MFMA_DEFAULT 1
 #endif
 #ifndef IVC_ME_TILE_PREFETCH
 #define IVC_ME_TILE_PREFETCH 0
@@ -967,6 +972,15 @@ __global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const
   }
 }
 
+// IVC_ME_MFMA: 1 = the matrix-core +-16 search (ivc_me_mfma.hip), 0 = the dot4 tiled search
+bool me_use_mfma() {
+  static const bool v = [] {
+    const char* e = getenv("IVC_ME_MFMA");
+    return e ? atoi(e) != 0 : IVC_ME_MFMA_DEFAULT != 0;
+  }();
+  return v;
+}
+
 hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, int64_t nframes,
                                   int64_t H, int64_t W, int sr, int mode, int64_t* mv,
                                   hipStream_t s) {
@@ -979,6 +993,10 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
   if (mode == IVC_ME_EXACT_U8) {
     if (dtype != IVC_U8) return hipErrorInvalidValue;
     // the dot4 searches address a frame's S2 plane (4 B per pixel) with 32-bit buffer offsets
+    // the matrix-core +-16 search needs no S2 plane: the whole batch in one launch
+    if (IVC_ME_TILE && sr == 16 && me_use_mfma() && launch_me_mfma16((const uint8_t*)ref, (const uint8_t*)cur,
+                                                                     nframes, h, w, mv, s))
+      return hipGetLastError();
     if ((sr == 4 || sr == 8 || sr == 16) && H * W * 4 < ((int64_t)1 << 31)) {
       // Frame pairs go in chunks of about IVC_ME_CHUNK_BYTES of S2 (one int32 per reference
       // pixel, stream-ordered scratch; at least one frame): a chunk the size of the 256 MB
