@@ -6,9 +6,9 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-IVC_ME_MFMA=1 timeout -k 10 600 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread \
+[ -n "$SKIP_TESTS" ] || IVC_ME_MFMA=1 timeout -k 10 600 python -u -m pytest tests -m gpu -v -x --timeout 300 --timeout-method thread \
   -p no:cacheprovider -k "${ME_TESTS:-me_ or sr16 or inter or videocodec or smoke}" > gpurun_out/pytest_me.log 2>&1 || { tail -40 gpurun_out/pytest_me.log; exit 1; }
-tail -2 gpurun_out/pytest_me.log
+[ -n "$SKIP_TESTS" ] || tail -2 gpurun_out/pytest_me.log
 INTER_ONLY="--no-intra --no-symbols --no-f64 --no-class-api --no-sharded --no-cpu --no-pmc --no-luma --inter-steps 5"
 for mode in ${MODES:-0 1 0 1}; do            # m or m:var (IVC_ME_VAR: ivc_me_mfma.hip)
   m=${mode%%:*}; var=0; [[ $mode == *:* ]] && var=${mode#*:}
