@@ -569,10 +569,18 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
     nsym = int(offs[-1].item())
     sym = torch.empty(nsym, dtype=torch.int32, device=dev)
     zwall, zms = timed(dist, lambda: D.zerorun_encode(blocks, offs, sym), 3, 1)
-    # the same stream straight from the pixels (fused: the coefficients never reach HBM)
+    # the same stream straight from the pixels (fused: the coefficients never reach HBM), with
+    # the stream's guarded histogram accumulated by the emission pass itself (the Huffman
+    # exchange then needs no pass over the stream)
     sym2 = torch.empty(nsym, dtype=torch.int32, device=dev)
     nsym_d = torch.zeros(1, dtype=torch.int64, device=dev)
-    fwall, fms = timed(dist, lambda: D.intra_symbols(frames, table, sym2, nsym_d), 3, 1)
+    hist = torch.zeros(HIST_BINS + 2, dtype=torch.int64, device=dev)
+
+    def fused_step():
+        hist.zero_()
+        D.intra_symbols(frames, table, sym2, nsym_d, hist=hist, hist_lo=HIST_LO - 1)
+
+    fwall, fms = timed(dist, fused_step, 3, 1)
     fused_same = bool(int(nsym_d.item()) == nsym) and bool(torch.equal(sym, sym2))
     del sym2
     if verify is not None:
@@ -591,11 +599,9 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
     fallback = {"used": False}
 
     def exchange():
-        # one pass over the stream: a histogram over the fixed range [HIST_LO, HIST_LO +
-        # HIST_BINS) with a guard bin at each end, one all-gather; the alphabet bounds
-        # (min - 20, max + 21: intracodec.py:161-166) come from its first and last nonzero bins
-        hist = torch.zeros(HIST_BINS + 2, dtype=torch.int64, device=dev)
-        D.histogram(sym, HIST_LO - 1, hist)
+        # the emission pass's histogram over the fixed range [HIST_LO, HIST_LO + HIST_BINS) with
+        # a guard bin at each end, one all-gather; the alphabet bounds (min - 20, max + 21:
+        # intracodec.py:161-166) come from its first and last nonzero bins
         g = global_histogram(hist).cpu().numpy()
         bnd = bounds_from_histogram(g, HIST_LO)
         if bnd is not None:
@@ -650,12 +656,18 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
             want = O.histogram(pre.cpu().numpy(), HIST_LO - 1, HIST_BINS + 2)
             check_equal(hp.cpu().numpy(), want, "exchange histogram of a prefix vs oracle",
                         verify["failures"])
+        hs = torch.zeros(HIST_BINS + 2, dtype=torch.int64, device=dev)
+        D.histogram(sym, HIST_LO - 1, hs)
+        check_equal(hist.cpu().numpy(), hs.cpu().numpy(), "emission-pass histogram vs a pass "
+                    "over the stream", verify["failures"])
         verify["checked"].append("exchange: bounds == stream min/max -20/+21, histogram == the "
-                                 "two-pass histogram; a 16M-symbol prefix vs the oracle")
+                                 "two-pass histogram; the emission pass's histogram == a histogram "
+                                 "pass over the stream; a 16M-symbol prefix vs the oracle")
     result["exchange"] = {
         "alphabet": [b0, b1], "bins": b1 - b0 - 1, "symbols": int(counts.sum()),
         "entropy_bits_per_symbol": round(entropy_bits(pmf), 4), "ms": round(exchange_ms, 3),
-        "passes_over_stream": 1 if not fallback["used"] else 3,
+        "passes_over_stream": 0 if not fallback["used"] else 2,
+        "histogram": "accumulated by the image2symbols emission pass (LDS bins, flushed per workgroup)",
         "collective": (f"all_gather_into_tensor ({coll_name(dist)}), {HIST_BINS + 2} int64 bins"
                        if not fallback["used"] else f"all_reduce + all_gather ({coll_name(dist)})")
         if dist is not None else "none (1 rank)"}

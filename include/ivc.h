@@ -310,6 +310,14 @@ int ivc_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, in
 int ivc_intra_symbols_dev(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                           int C, const double* table, int32_t eob, int32_t* out,
                           int64_t capacity, int64_t* nsym, void* stream);
+/* ivc_intra_symbols_dev that also accumulates the clamped histogram of the whole stream (also
+ * the symbols past capacity) onto hist[clamp(v - hist_lo, 0, hist_n - 1)] (device
+ * int64[hist_n]; nothing is added when capacity = 0, which runs no emission pass): the counts IntraCodec.train_huffman_from_image's stats_marg takes
+ * (intracodec.py:160-166, entropy.py:6-29) with no further pass over the stream.          */
+int ivc_intra_symbols_hist_dev(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
+                               int C, const double* table, int32_t eob, int32_t* out,
+                               int64_t capacity, int64_t* nsym, int64_t* hist, int32_t hist_lo,
+                               int32_t hist_n, void* stream);
 /* mm[0] = min, mm[1] = max of n int32 symbols (INT32_MAX, INT32_MIN when n = 0): the
  * Huffman alphabet bounds of IntraCodec.train_huffman_from_image (intracodec.py:161-163). */
 int ivc_minmax_i32(const int32_t* sym, int64_t n, int32_t* mm);

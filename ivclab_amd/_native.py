@@ -92,6 +92,8 @@ _SIGS = {
     "ivc_rgb2gray_dev": ([_P, _ct.c_int, _L, _L, _P, _P], _I),
     "ivc_intra_symbols": ([_P, _ct.c_int, _L, _L, _L, _ct.c_int, _P, _ct.c_int32, _P, _L, _P], _I),
     "ivc_intra_symbols_dev": ([_P, _ct.c_int, _L, _L, _L, _ct.c_int, _P, _ct.c_int32, _P, _L, _P, _P], _I),
+    "ivc_intra_symbols_hist_dev": ([_P, _ct.c_int, _L, _L, _L, _ct.c_int, _P, _ct.c_int32, _P, _L, _P,
+                                    _P, _ct.c_int32, _ct.c_int32, _P], _I),
     "ivc_minmax_i32": ([_P, _L, _P], _I),
     "ivc_minmax_i32_dev": ([_P, _L, _P, _P], _I),
     "ivc_zerorun_encode": ([_P, _L, _ct.c_int32, _ct.c_int32, _ct.c_int32, _P, _L, _P], _I),

@@ -1041,6 +1041,22 @@ int ivc_intra_symbols_dev(const void* img, int dtype, int64_t nframes, int64_t H
                                          (hipStream_t)stream), "intra_symbols");
 }
 
+int ivc_intra_symbols_hist_dev(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
+                               int C, const double* table, int32_t eob, int32_t* out,
+                               int64_t capacity, int64_t* nsym, int64_t* hist, int32_t hist_lo,
+                               int32_t hist_n, void* stream) {
+  TRY(check_frames(nframes, H, W, "intra_symbols_hist"));
+  CHECK(C == 1 || C == 3, IVC_E_SHAPE, "intra_symbols_hist: C must be 1 or 3");
+  CHECK(dtype == IVC_U8, IVC_E_DTYPE, "intra_symbols_hist: uint8 frames only");
+  CHECK(capacity >= 0 && nsym, IVC_E_ARG, "intra_symbols_hist: need capacity >= 0 and nsym");
+  CHECK(hist && hist_n >= 1, IVC_E_ARG, "intra_symbols_hist: need a histogram of >= 1 bin");
+  QTab t;
+  TRY(load_table(table, &t));
+  return dev_launch(launch_intra_symbols(img, dtype, nframes, H, W, C, t, eob, out, capacity, nsym,
+                                         (hipStream_t)stream, hist, hist_lo, hist_n),
+                    "intra_symbols_hist");
+}
+
 int ivc_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W, int C,
                       const double* table, int32_t eob, int32_t* out, int64_t capacity,
                       int64_t* nsym) {

@@ -64,7 +64,8 @@ hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* 
                                      hipStream_t s);
 hipError_t launch_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                                 int C, const QTab& t, int32_t eob, int32_t* out, int64_t capacity,
-                                int64_t* nsym, hipStream_t s);
+                                int64_t* nsym, hipStream_t s, int64_t* hist = nullptr,
+                                int32_t hist_lo = 0, int32_t hist_n = 0);
 int64_t zerorun_scratch_bytes(int64_t nblk);
 hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, int B,
                                   void* scratch, int64_t* off, hipStream_t s);

@@ -316,6 +316,11 @@ struct FusedArgs {
   int32_t* zr_out;
   int64_t zr_cap;
   int32_t zr_eob;
+  // OUT_SYMBOLS, optional: the clamped histogram of the emitted stream accumulated onto
+  // zr_hist[clamp(v - zr_hist_lo, 0, zr_hist_n - 1)] (int64 counts), so the Huffman-table
+  // exchange needs no pass over the stream
+  unsigned long long* zr_hist;
+  int32_t zr_hist_lo, zr_hist_n;
   // store pacing (OUT_COEFS): slot s of wave w (of W) stores no earlier than
   // (*pace_t0 + (s * pace_d + w * pace_d / W) / 256) on the 100 MHz s_memrealtime clock;
   // pace_d = 0: unpaced
@@ -726,9 +731,25 @@ constexpr int ZR_WIN = XS_PITCH * 8 * 8 / 4;   // int32 symbols in a wave's tran
 // stream with consecutive-address stores before a block-plane that might not fit.  Per
 // group: two ds_write per block-plane instead of one per (plane, coefficient) slot and
 // window pass (the per-lane form below): 11.6 vs 13.3 ms for 256 x 4K (same-process A/B).
+// The stream's histogram rides along (a.zr_hist): each block-plane's nonzero values and run
+// lengths go to the workgroup's LDS bins (values in [-ZH_HALF, ZH_HALF); others straight to the
+// global histogram), its runs' 0 symbols and its EOB to two per-wave counters; the kernel adds
+// the bins and counters to the global histogram at its end.
+constexpr int ZH_HALF = 512, ZH_BINS = 2 * ZH_HALF;
+struct ZrHistAcc {
+  uint32_t* bins;      // workgroup LDS bins (nullptr: no histogram)
+  uint32_t runs, eobs; // wave-uniform counts of the 0 symbols of runs and of EOBs
+};
+__device__ __forceinline__ void zr_hist_global(const FusedArgs& a, int64_t v, uint32_t w) {
+  int64_t k = v - a.zr_hist_lo;
+  k = k < 0 ? 0 : (k >= a.zr_hist_n ? a.zr_hist_n - 1 : k);
+  __hip_atomic_fetch_add(a.zr_hist + k, (unsigned long long)w, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int C, bool DUP>
 __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, int nb,
-                                              int64_t gbase) {
+                                              int64_t gbase, ZrHistAcc& H) {
   constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging
   constexpr int PITCH = os_pitch<C, DUP>();
   const int lane = threadIdx.x & 63;
@@ -783,6 +804,20 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
       w1[p] = nz || rs || lane == last1;
       v1[p] = nz || rs ? x : a.zr_eob;                      // x == 0 at a run start
       v2[p] = rs ? __builtin_ctzll(m >> lane) : a.zr_eob;
+      if (H.bins) {
+        // the block-plane's symbols besides its runs' 0s and its EOB: the nonzero values and
+        // the run lengths (plane 1 counts twice when plane 2 repeats it)
+        const uint32_t wgt = p == 1 ? R1 : 1;
+        H.runs += wgt * (uint32_t)__builtin_popcountll(st);
+        H.eobs += wgt;
+        if (nz || rs) {
+          const int u = nz ? x : v2[p];
+          if ((unsigned)(u + ZH_HALF) < (unsigned)ZH_BINS)
+            atomicAdd(H.bins + (u + ZH_HALF), wgt);
+          else
+            zr_hist_global(a, u, wgt);
+        }
+      }
     }
     // one window check per block (its <= 3 x 97 symbols always fit an empty window)
     int tb = 0;
@@ -811,9 +846,9 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
 
 template <int C, bool DUP, int OUTM>
 __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b, int r, int nb,
-                                         int64_t gid) {
+                                         int64_t gid, ZrHistAcc& H) {
   if constexpr (OUTM == OUT_SYMBOLS && IVC_ZR_EMIT2) {
-    zr_group_emit<C, DUP>(a, os, nb, a.zr_off[gid]);
+    zr_group_emit<C, DUP>(a, os, nb, a.zr_off[gid], H);
     return;
   }
   constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging
@@ -929,6 +964,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
   __shared__ double srq[FAST ? 192 : 1];
   __shared__ D sq[192];
+  __shared__ uint32_t zh[OUTM == OUT_SYMBOLS ? ZH_BINS : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   const int b = lane >> 3, r = lane & 7;
@@ -945,7 +981,15 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
     zp0 |= (uint32_t)(ZZ ? c_zz_order[i * 8 + r] : i * 8 + r) << (8 * i);
     zp1 |= (uint32_t)(ZZ ? c_zz_order[(i + 4) * 8 + r] : (i + 4) * 8 + r) << (8 * i);
   }
-  __syncthreads();  // tables only; the loop below never synchronises across waves
+  ZrHistAcc hacc{nullptr, 0u, 0u};
+  if constexpr (OUTM == OUT_SYMBOLS) {
+    if (a.zr_hist) {
+      for (int i = tid; i < ZH_BINS; i += 256) zh[i] = 0;
+      hacc.bins = zh;
+    }
+  }
+  __syncthreads();  // tables only; the loop below never synchronises across waves (but the
+                    // symbol histogram's bins are flushed after a barrier at the end)
 
   unsigned char* mine = lds + wave * L::BYTES;
   T* xs = reinterpret_cast<T*>(mine);
@@ -1020,7 +1064,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
           group_row<TI, C, NG>(ring[p], g, lane, v);
           encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
           if constexpr (!COEF) {
-            if (ex) zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, tp, g).nb, (int64_t)tp * NG + g);
+            if (ex) zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, tp, g).nb, (int64_t)tp * NG + g, hacc);
           }
           plt = tp;
           pg = g;
@@ -1061,7 +1105,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
         }
         encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
         if constexpr (!COEF)
-          zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, lt, g).nb, (int64_t)lt * NG + g);
+          zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, lt, g).nb, (int64_t)lt * NG + g, hacc);
         plt = lt;
         pg = g;
         have_prev = true;
@@ -1088,6 +1132,17 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
       if (nlate)
         __hip_atomic_fetch_min(blk + PACE_FIRST_LATE, (unsigned long long)first_late,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if constexpr (OUTM == OUT_SYMBOLS) {
+    if (a.zr_hist) {
+      __syncthreads();
+      for (int i = tid; i < ZH_BINS; i += 256)
+        if (zh[i]) zr_hist_global(a, i - ZH_HALF, zh[i]);
+      if (lane == 0) {
+        if (hacc.runs) zr_hist_global(a, 0, hacc.runs);
+        if (hacc.eobs) zr_hist_global(a, a.zr_eob, hacc.eobs);
+      }
     }
   }
 }
@@ -1559,6 +1614,9 @@ static FusedArgs make_fused_args(const void* img, const int64_t* mv, int32_t* ou
   a.zr_out = nullptr;
   a.zr_cap = 0;
   a.zr_eob = 0;
+  a.zr_hist = nullptr;
+  a.zr_hist_lo = 0;
+  a.zr_hist_n = 0;
   a.pace_t0 = nullptr;
   a.pace_d = 0;
   a.pace_early = 0;
@@ -1666,12 +1724,16 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
 
 hipError_t launch_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                                 int C, const QTab& t, int32_t eob, int32_t* out, int64_t capacity,
-                                int64_t* nsym, hipStream_t s) {
+                                int64_t* nsym, hipStream_t s, int64_t* hist, int32_t hist_lo,
+                                int32_t hist_n) {
   if (dtype != IVC_U8 || (C != 1 && C != 3)) return hipErrorInvalidValue;
   FusedArgs a = make_fused_args(img, nullptr, nullptr, nframes, H, W, 0, t);
   a.zr_out = out;
   a.zr_cap = capacity;
   a.zr_eob = eob;
+  a.zr_hist = hist_n > 0 ? reinterpret_cast<unsigned long long*>(hist) : nullptr;
+  a.zr_hist_lo = hist_lo;
+  a.zr_hist_n = hist_n;
   if (nframes <= 0 || H <= 0 || W <= 0) return hipMemsetAsync(nsym, 0, 8, s);
   if (nframes * (int64_t)a.h * a.tpr >= (1LL << 31)) return hipErrorInvalidValue;
   const bool cm = needs_magnitude_check(t);

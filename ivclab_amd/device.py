@@ -137,11 +137,13 @@ def minmax(sym, mm, stream=None):
                                        _stream(stream)), "minmax")
 
 
-def intra_symbols(frames, table, out, nsym, eob=4000, stream=None):
+def intra_symbols(frames, table, out, nsym, eob=4000, stream=None, hist=None, hist_lo=0):
     """u8 frames [F, H, W] or [F, H, W, C] -> the zero-run symbol stream of their quantised
     zig-zag blocks (IntraCodec.image2symbols without colour conversion, one fused pass per
     frame batch; the coefficients never reach memory).  out: int32 (written up to its
-    length), nsym: int64 device scalar receiving the stream length.  Asynchronous."""
+    length), nsym: int64 device scalar receiving the stream length.  hist (optional, int64
+    [n]): the emitted stream's histogram is accumulated onto hist[clamp(v - hist_lo, 0,
+    n - 1)] by the emission pass itself.  Asynchronous."""
     import torch
     _contig(frames, "frames"); _contig(out, "out"); _contig(nsym, "nsym")
     if frames.dtype != torch.uint8 or out.dtype != torch.int32 or nsym.dtype != torch.int64:
@@ -149,9 +151,22 @@ def intra_symbols(frames, table, out, nsym, eob=4000, stream=None):
     F, H, W = frames.shape[:3]
     C = frames.shape[3] if frames.dim() == 4 else 1
     t = N.table_arg(table)
-    N.check(N.lib().ivc_intra_symbols_dev(frames.data_ptr(), N.DTYPE_CODE[np.dtype(np.uint8)], F, H,
-                                          W, C, N.ptr(t), int(eob), out.data_ptr(), out.numel(),
-                                          nsym.data_ptr(), _stream(stream)), "intra_symbols")
+    if hist is None:
+        N.check(N.lib().ivc_intra_symbols_dev(frames.data_ptr(), N.DTYPE_CODE[np.dtype(np.uint8)], F,
+                                              H, W, C, N.ptr(t), int(eob), out.data_ptr(),
+                                              out.numel(), nsym.data_ptr(), _stream(stream)),
+                "intra_symbols")
+        return
+    _contig(hist, "hist")
+    if hist.dtype != torch.int64 or hist.dim() != 1 or hist.numel() < 1:
+        raise ValueError("intra_symbols: hist must be a 1-D int64 tensor")
+    if not -(1 << 31) <= int(hist_lo) < (1 << 31) or hist.numel() >= (1 << 31):
+        raise ValueError("intra_symbols: hist_lo / hist size out of int32 range")
+    N.check(N.lib().ivc_intra_symbols_hist_dev(frames.data_ptr(), N.DTYPE_CODE[np.dtype(np.uint8)], F,
+                                               H, W, C, N.ptr(t), int(eob), out.data_ptr(),
+                                               out.numel(), nsym.data_ptr(), hist.data_ptr(),
+                                               int(hist_lo), hist.numel(), _stream(stream)),
+            "intra_symbols")
 
 
 def intra_decode_image(q, table, out, unzigzag=True, to_rgb=False, stream=None):

@@ -1038,6 +1038,45 @@ def test_intra_symbols_device_and_4k():
     assert np.array_equal(short.cpu().numpy(), want[:12345])
 
 
+@pytest.mark.parametrize("case", ["s1", "s007", "custom", "rgb", "ragged"])
+def test_intra_symbols_emission_histogram(case):
+    """The emission pass's clamped histogram of the stream (ivc_intra_symbols_hist_dev) equals
+    the oracle's histogram of the oracle stream: a wide guarded range (values past +-512 take
+    the global path at scale 0.07), a narrow one (most symbols, EOB included, clamp into the end
+    bins), accumulation onto existing counts, and a capacity-cut stream (counted whole)."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(len(case) * 7 + 3)
+    F, H, W, C = 2, 48, 136, 1
+    scale = {"s1": 1.0, "s007": 0.07}.get(case, 0.5)
+    if case == "rgb":
+        C = 3
+    if case == "ragged":
+        W = 264
+    img = rng.integers(0, 256, (F, H, W, C), dtype=np.uint8)
+    img[:, :16] = img[:, :1, :1]
+    table = PatchQuant(scale).get_quantization_table().astype(np.float64)
+    if case == "custom":
+        table[2] *= 1.61
+    want = _zr_chain(img, table)
+    fr = torch.from_numpy(img if C == 3 else img[..., 0]).cuda()
+    nsym = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out = torch.empty(want.size, dtype=torch.int32, device="cuda")
+    for lo, n in [(-4097, 8194), (-3, 9)]:
+        hist = torch.zeros(n, dtype=torch.int64, device="cuda")
+        D.intra_symbols(fr, table, out, nsym, hist=hist, hist_lo=lo)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), want)
+        ref = O.histogram(want, lo, n)
+        assert np.array_equal(hist.cpu().numpy(), ref), (case, lo, n)
+        if lo == -3:
+            D.intra_symbols(fr, table, out[:want.size // 3], nsym, hist=hist, hist_lo=lo)
+            torch.cuda.synchronize()
+            assert np.array_equal(hist.cpu().numpy(), 2 * ref), "accumulated / capacity-cut"
+    if case == "s007":                              # the out-of-LDS-range path ran
+        assert (np.abs(want[want != 4000]) >= 512).any()
+
+
 @pytest.mark.parametrize("shift", [1, 2, 3])
 def test_intra_symbols_unaligned_stream(shift):
     """The fused emit's 16-byte stores when the output view starts 4/8/12 bytes past a 16-byte
