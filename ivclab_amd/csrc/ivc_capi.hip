@@ -682,11 +682,11 @@ static int symbols2image_enqueue(const int32_t* sym, int64_t nsym, int64_t nfram
                                  int64_t W, int C, const QTab& t, int32_t eob, int to_rgb,
                                  double* out, int64_t* err, void* coef, void* scratch,
                                  hipStream_t s) {
-  const int64_t nblk = nframes * (H / 8) * (W / 8) * C;
-  TRY(dev_launch(launch_zerorun_decode(sym, nsym, nblk, 64, eob, (int32_t*)coef, scratch, err, s),
-                 "symbols2image: zerorun_decode"));
-  return dev_launch(launch_intra_decode_image((const int32_t*)coef, nframes, H, W, C, t, 1, to_rgb,
-                                              out, s), "symbols2image: intra_decode_image");
+  return dev_launch(launch_symbols2image(sym, nsym, nframes, H, W, C, t, eob, to_rgb, out,
+                                         (int32_t*)coef, scratch, err, s), "symbols2image");
+}
+static int64_t s2i_scratch_bytes(int64_t nsym, int64_t nframes, int64_t H, int64_t W) {
+  return sym_image_scratch_bytes(nsym, nframes * (H / 8) * ((W / 8 + 7) / 8));
 }
 
 int ivc_symbols2image_dev(const int32_t* sym, int64_t nsym, int64_t nframes, int64_t H, int64_t W,
@@ -702,7 +702,7 @@ int ivc_symbols2image_dev(const int32_t* sym, int64_t nsym, int64_t nframes, int
   const int64_t nblk = nframes * (H / 8) * (W / 8) * C;
   void *coef = nullptr, *scratch = nullptr;
   hipError_t e = scratch_alloc(&coef, (size_t)nblk * 256, s);
-  if (e == hipSuccess) e = scratch_alloc(&scratch, (size_t)zr_decode_scratch_bytes(nsym), s);
+  if (e == hipSuccess) e = scratch_alloc(&scratch, (size_t)s2i_scratch_bytes(nsym, nframes, H, W), s);
   if (e != hipSuccess) {
     if (coef) (void)hipFreeAsync(coef, s);
     return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
@@ -727,7 +727,7 @@ int ivc_symbols2image(const int32_t* sym, int64_t nsym, int64_t nframes, int64_t
   TRY(st.open());
   const size_t ob = (size_t)(nframes * H * W) * 3 * 8;
   const int32_t* d_sym = (const int32_t*)st.in(sym, (size_t)nsym * 4);
-  void* scratch = st.alloc((size_t)zr_decode_scratch_bytes(nsym));
+  void* scratch = st.alloc((size_t)s2i_scratch_bytes(nsym, nframes, H, W));
   void* coef = st.alloc((size_t)nblk * 256);
   double* d_out = (double*)st.alloc(ob);
   int64_t* d_err = (int64_t*)st.alloc(3 * 8);

@@ -39,6 +39,7 @@ struct DecArgs {
   int64_t ngroups;       // groups of <= 8 blocks (DEC_IMAGE: groups never cross a block row)
   int w, gpr;            // DEC_IMAGE: blocks per block row, groups per block row
   int64_t W3;            // DEC_IMAGE: doubles per image row (W * 3)
+  const int* skip;       // optional: the kernel does nothing when *skip != 0
 };
 
 typedef unsigned int dec_u32x4 __attribute__((ext_vector_type(4)));
@@ -95,6 +96,106 @@ __device__ __forceinline__ void dec_load(const DecArgs& a, int64_t g, int lane, 
     v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (j * 64 + lane) * 16, 0, 0);
 }
 
+// Dequantise + IDCT (+ RGB) of one group staged in LDS (qs: block-plane b * C + p at
+// qs + (b * C + p) * DQ_PITCH, zig-zag or raster order inside) and its output: DEC_BLOCKS
+// [nblk][3][8][8] or DEC_IMAGE rows.  Shared by intra_decode_kernel (coefficients from HBM) and
+// sym_image_kernel (coefficients expanded from the zero-run stream).
+template <int C, int OUTL, bool RGB>
+__device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup& G,
+                                               const int32_t* qs, double* xs, const double* tq,
+                                               const uint32_t* pos, int b, int r, int lane) {
+  double o[RGB || OUTL == DEC_IMAGE ? 3 : 1][8];
+  int32_t qv[8];
+#pragma unroll
+  for (int p = 0; p < 3; ++p) {
+    if (C == 3 || p == 0) {
+      const int32_t* qb = qs + (b * C + (C == 3 ? p : 0)) * DQ_PITCH;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qv[k] = qb[(pos[k >> 2] >> (8 * (k & 3))) & 0xff];
+    }
+    double x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k)   // patchquant.py:77-78: int32 * table (float64), truncated
+      x[k] = (double)np_to_i32<double>((double)qv[k] * tq[p * 64 + r * 8 + k]);
+    dct3_line<double>(x, 0.25, true);                 // axis -1 (row r)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xs[b * 72 + r * 9 + k] = x[k];
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = xs[b * 72 + i * 9 + r];
+    __builtin_amdgcn_wave_barrier();
+    dct3_line<double>(x, 0.25, true);                 // axis -2 (column r)
+    if constexpr (OUTL == DEC_BLOCKS) {
+      // plane p of the group's blocks: [b][i][r], 8 x 512 B, block b's plane at
+      // out + ((blk0 + b) * 3 + p) * 64
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xs[b * 64 + i * 8 + r] = x[i];
+      __builtin_amdgcn_wave_barrier();
+      const __amdgpu_buffer_rsrc_t ro = dec_rsrc(a.out + (G.blk0 * 3 + p) * 64, (uint32_t)G.nb * 1536u);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = j * 64 + lane;                  // block c / 32, chunk c % 32
+        const dec_u32x4 v = *reinterpret_cast<const dec_u32x4*>(xs + (c >> 5) * 64 + (c & 31) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(v, ro, (c >> 5) * 1536 + (c & 31) * 16, 0,
+                                               IVC_DEC_STORE_AUX);
+      }
+      __builtin_amdgcn_wave_barrier();
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[p][i] = x[i];
+    }
+  }
+  if constexpr (OUTL == DEC_IMAGE) {
+    if constexpr (RGB) {
+      // color.py:40-63, elementwise in float64; np.clip(v, 0, 255) keeps NaN
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const double Y = o[0][i], Cb = o[1][i] - 128.0, Cr = o[2][i] - 128.0;
+        double v[3];
+        v[0] = Y + 1.402 * Cr;
+        v[1] = (Y - 0.344136 * Cb) - 0.714136 * Cr;
+        v[2] = Y + 1.772 * Cb;
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+          o[c][i] = v[c] != v[c] ? v[c] : (v[c] < 0.0 ? 0.0 : (v[c] > 255.0 ? 255.0 : v[c]));
+      }
+    }
+    // two image rows at a time: stage [ri][px = 8 b + r][p], then 16-byte stores of the
+    // rows' nb * 192 contiguous bytes each
+    const int nb12 = G.nb * 12;
+    double* rowp = a.out + (G.row * 8) * a.W3 + (int64_t)G.bx0 * 24;
+#pragma unroll
+    for (int i0 = 0; i0 < 8; i0 += 2) {
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) xs[(ri * 64 + lane) * 3 + p] = o[p][i0 + ri];
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int ri = 0; ri < 2; ++ri) {
+        const __amdgpu_buffer_rsrc_t ro = dec_rsrc(rowp + (i0 + ri) * a.W3, (uint32_t)nb12 * 16u);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int c = j * 64 + lane;                // chunk of this row (96 at most)
+          const dec_u32x4 v = *reinterpret_cast<const dec_u32x4*>(xs + ri * 192 + c * 2);
+          __builtin_amdgcn_raw_buffer_store_b128(v, ro, c < 96 ? c * 16 : 0x40000000, 0,
+                                                 IVC_DEC_STORE_AUX);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// raster positions gathered by lane (b, r): row r of its block, as stored in the staging
+template <bool ZZ>
+__device__ __forceinline__ void dec_gather_pos(int r, uint32_t* pos) {
+  pos[0] = pos[1] = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    pos[k >> 2] |= (uint32_t)(ZZ ? c_dec_zz_order[r * 8 + k] : r * 8 + k) << (8 * (k & 3));
+}
+
 template <int C, bool ZZ, int OUTL, bool RGB>
 __global__ __launch_bounds__(256) void intra_decode_kernel(DecArgs a, QTab t) {
   static_assert(OUTL == DEC_IMAGE || !RGB, "RGB output needs the image layout");
@@ -106,12 +207,10 @@ __global__ __launch_bounds__(256) void intra_decode_kernel(DecArgs a, QTab t) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = lane >> 3, r = lane & 7;
+  if (a.skip && *a.skip) return;
   for (int i = tid; i < 192; i += 256) tq[i] = t.q[i];
-  // raster positions gathered by this lane (row r of its block), as stored in the input
-  uint32_t pos[2] = {0, 0};
-#pragma unroll
-  for (int k = 0; k < 8; ++k)
-    pos[k >> 2] |= (uint32_t)(ZZ ? c_dec_zz_order[r * 8 + k] : r * 8 + k) << (8 * (k & 3));
+  uint32_t pos[2];
+  dec_gather_pos<ZZ>(r, pos);
   __syncthreads();   // the table only: the loop never synchronises across waves
 
   int32_t* qs = qs_all + wave * QS;
@@ -131,89 +230,160 @@ __global__ __launch_bounds__(256) void intra_decode_kernel(DecArgs a, QTab t) {
       *reinterpret_cast<dec_u32x4*>(qs + (c >> 4) * DQ_PITCH + (c & 15) * 4) = raw[j];
     }
     __builtin_amdgcn_wave_barrier();
-    double o[RGB || OUTL == DEC_IMAGE ? 3 : 1][8];
-    int32_t qv[8];
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      if (C == 3 || p == 0) {
-        const int32_t* qb = qs + (b * C + (C == 3 ? p : 0)) * DQ_PITCH;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) qv[k] = qb[(pos[k >> 2] >> (8 * (k & 3))) & 0xff];
-      }
-      double x[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k)   // patchquant.py:77-78: int32 * table (float64), truncated
-        x[k] = (double)np_to_i32<double>((double)qv[k] * tq[p * 64 + r * 8 + k]);
-      dct3_line<double>(x, 0.25, true);                 // axis -1 (row r)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) xs[b * 72 + r * 9 + k] = x[k];
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int i = 0; i < 8; ++i) x[i] = xs[b * 72 + i * 9 + r];
-      __builtin_amdgcn_wave_barrier();
-      dct3_line<double>(x, 0.25, true);                 // axis -2 (column r)
-      if constexpr (OUTL == DEC_BLOCKS) {
-        // plane p of the group's blocks: [b][i][r], 8 x 512 B, block b's plane at
-        // out + ((blk0 + b) * 3 + p) * 64
-#pragma unroll
-        for (int i = 0; i < 8; ++i) xs[b * 64 + i * 8 + r] = x[i];
-        __builtin_amdgcn_wave_barrier();
-        const __amdgpu_buffer_rsrc_t ro = dec_rsrc(a.out + (G.blk0 * 3 + p) * 64, (uint32_t)G.nb * 1536u);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int c = j * 64 + lane;                  // block c / 32, chunk c % 32
-          const dec_u32x4 v = *reinterpret_cast<const dec_u32x4*>(xs + (c >> 5) * 64 + (c & 31) * 2);
-          __builtin_amdgcn_raw_buffer_store_b128(v, ro, (c >> 5) * 1536 + (c & 31) * 16, 0,
-                                                 IVC_DEC_STORE_AUX);
-        }
-        __builtin_amdgcn_wave_barrier();
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) o[p][i] = x[i];
-      }
-    }
-    if constexpr (OUTL == DEC_IMAGE) {
-      if constexpr (RGB) {
-        // color.py:40-63, elementwise in float64; np.clip(v, 0, 255) keeps NaN
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const double Y = o[0][i], Cb = o[1][i] - 128.0, Cr = o[2][i] - 128.0;
-          double v[3];
-          v[0] = Y + 1.402 * Cr;
-          v[1] = (Y - 0.344136 * Cb) - 0.714136 * Cr;
-          v[2] = Y + 1.772 * Cb;
-#pragma unroll
-          for (int c = 0; c < 3; ++c)
-            o[c][i] = v[c] != v[c] ? v[c] : (v[c] < 0.0 ? 0.0 : (v[c] > 255.0 ? 255.0 : v[c]));
-        }
-      }
-      // two image rows at a time: stage [ri][px = 8 b + r][p], then 16-byte stores of the
-      // rows' nb * 192 contiguous bytes each
-      const int nb12 = G.nb * 12;
-      double* rowp = a.out + (G.row * 8) * a.W3 + (int64_t)G.bx0 * 24;
-#pragma unroll
-      for (int i0 = 0; i0 < 8; i0 += 2) {
-#pragma unroll
-        for (int ri = 0; ri < 2; ++ri)
-#pragma unroll
-          for (int p = 0; p < 3; ++p) xs[(ri * 64 + lane) * 3 + p] = o[p][i0 + ri];
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int ri = 0; ri < 2; ++ri) {
-          const __amdgpu_buffer_rsrc_t ro = dec_rsrc(rowp + (i0 + ri) * a.W3, (uint32_t)nb12 * 16u);
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const int c = j * 64 + lane;                // chunk of this row (96 at most)
-            const dec_u32x4 v = *reinterpret_cast<const dec_u32x4*>(xs + ri * 192 + c * 2);
-            __builtin_amdgcn_raw_buffer_store_b128(v, ro, c < 96 ? c * 16 : 0x40000000, 0,
-                                                   IVC_DEC_STORE_AUX);
-          }
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-    }
+    dec_group_math<C, OUTL, RGB>(a, G, qs, xs, tq, pos, b, r, lane);
 #pragma unroll
     for (int j = 0; j < NCH; ++j) raw[j] = nxt[j];
+  }
+}
+
+// ---- zero-run symbols -> image, fused (IntraCodec.symbols2image, intracodec.py:84-146 with
+// zerorun.py:44-88 in front): for a well-formed stream (the fast decoder's conditions,
+// ivc_entropy.hip), the coefficients never reach HBM.  A wave takes a group of 8 blocks of a
+// block row — C x nb consecutive block-planes of the stream, starting at gstart[g] (found
+// from the EOB bit mask by sym_locate_kernel) — and expands its symbols 64 at a time straight
+// into the zeroed LDS staging of dec_group_math: lane j takes symbol j of the chunk; its slot
+// type follows from the previous symbol (a run-length slot iff it is 0), its coefficient count
+// (1 for a nonzero value, the run length for a 0, none for run-length and EOB slots) and its
+// EOB flag are prefix-summed across the wave in one packed DPP scan, and a DPP max-scan of the
+// EOB lanes' coefficient offsets gives each lane's block-plane start, so a nonzero value lands
+// at (its block-plane, offset - start).  Any violation (a block-plane past 64 coefficients, a
+// group whose EOB count or bounds do not match) sets `fail`, and the general path (zero-run
+// decode into coefficients + intra_decode_kernel, gated on the device) overwrites the image.
+// HBM per pixel: the stream's ~6.8 B (cfg3: 4 B/symbol) + 24 B of RGB float64.
+__device__ __forceinline__ int dec_wave_incl_sum(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return v;
+}
+// inclusive max-scan over the wave for v >= 0 (0 is the identity)
+__device__ __forceinline__ int dec_wave_incl_max(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
+  return v;
+}
+
+struct SymImageArgs {
+  const int32_t* sym;
+  int64_t n;
+  int32_t eob;
+  const int64_t* gstart;   // [ngroups + 1]: first symbol of each group (-1: not found)
+  int* fail;
+};
+
+template <int C, bool RGB>
+__global__ __launch_bounds__(256) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t) {
+  constexpr int QS = 8 * C * DQ_PITCH;
+  __shared__ __attribute__((aligned(16))) int32_t qs_all[4 * QS];
+  __shared__ __attribute__((aligned(16))) double xs_all[4 * DX_WAVE];
+  __shared__ double tq[192];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = lane >> 3, r = lane & 7;
+  for (int i = tid; i < 192; i += 256) tq[i] = t.q[i];
+  uint32_t pos[2];
+  dec_gather_pos<true>(r, pos);
+  __syncthreads();   // the table only
+
+  int32_t* qs = qs_all + wave * QS;
+  double* xs = xs_all + wave * DX_WAVE;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  bool bad = false;
+  for (int64_t g = (int64_t)blockIdx.x * 4 + wave; g < a.ngroups; g += nw) {
+    const DecGroup G = dec_group<DEC_IMAGE>(a, g);
+    const int64_t S = z.gstart[g], E = z.gstart[g + 1];
+    const int nbp = C * G.nb;                          // block-planes (EOBs) of the group
+    // zero the staging (C x 8 rows of DQ_PITCH int32)
+#pragma unroll
+    for (int j = 0; j < (QS / 4 + 63) / 64; ++j) {
+      const int c = j * 64 + lane;
+      if (c < QS / 4) *reinterpret_cast<dec_u32x4*>(qs + 4 * c) = dec_u32x4{0, 0, 0, 0};
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (S < 0 || E <= S || E > z.n || E - S > (int64_t)nbp * 130) {
+      bad = true;                                      // wave-uniform
+    } else {
+      const int len = (int)(E - S);
+      const __amdgpu_buffer_rsrc_t rs = dec_rsrc(z.sym + S, (uint32_t)len * 4u);
+      int cur = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0);
+      int prevc = 1;          // the symbol before the chunk (the group starts at a value slot)
+      int pcarry = 0;         // coefficients of the group before the chunk
+      int bpcarry = 0;        // EOBs before the chunk
+      int basecarry = 0;      // coefficient offset at which the current block-plane starts
+      for (int c0 = 0; c0 < len; c0 += 64) {
+        const int nxtv = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, (c0 + 64 + lane) * 4, 0, 0);
+        const int nxt0 = __builtin_amdgcn_readfirstlane(nxtv);
+        const int prv = __builtin_amdgcn_update_dpp(prevc, cur, 0x138, 0xf, 0xf, false);  // wave_shr:1
+        const int nx = __builtin_amdgcn_update_dpp(nxt0, cur, 0x130, 0xf, 0xf, false);    // wave_shl:1
+        const bool valid = c0 + lane < len;
+        const bool rl = prv == 0;                        // a run-length slot
+        const bool eobf = valid && !rl && cur == z.eob;
+        const bool isval = valid && !rl && !eobf;
+        const int run = nx < 1 ? 1 : (nx > 4095 ? 4095 : nx);
+        const int cc = isval ? (cur == 0 ? run : 1) : 0;
+        const int packed = (eobf ? (1 << 20) : 0) | cc;
+        const int incl = dec_wave_incl_sum(packed);
+        const int excl = incl - packed;
+        const int pex = pcarry + (excl & 0xfffff);     // this slot's coefficient offset
+        const int bp = bpcarry + (excl >> 20);          // its block-plane
+        const int mx = dec_wave_incl_max(eobf ? pex : 0);
+        int base = __builtin_amdgcn_update_dpp(0, mx, 0x138, 0xf, 0xf, false);  // exclusive
+        base = max(base, basecarry);
+        const int off = pex - base;                      // offset inside the block-plane
+        if (isval && cur != 0) {
+          if (off < 64 && bp < nbp) qs[bp * DQ_PITCH + off] = cur;
+          else bad = true;
+        }
+        if (eobf && (off > 64 || bp >= nbp)) bad = true;
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        pcarry += tot & 0xfffff;
+        bpcarry += tot >> 20;
+        basecarry = max(basecarry, __builtin_amdgcn_readlane(mx, 63));
+        prevc = __builtin_amdgcn_readlane(cur, 63);
+        cur = nxtv;
+      }
+      if (bpcarry != nbp) bad = true;
+      __builtin_amdgcn_wave_barrier();
+      dec_group_math<C, DEC_IMAGE, RGB>(a, G, qs, xs, tq, pos, b, r, lane);
+    }
+  }
+  if (__ballot(bad) && lane == 0) atomicOr(z.fail, 1);
+}
+
+// group starts from the EOB bit mask of zf_count (bit i of tile t: symbol t * 4096 + i is an
+// EOB slot) and tile_first (EOBs before each tile): the symbol after EOB number C * blk0(g) - 1
+// starts group g; one wave per 4096-symbol tile (lane = 64 symbols), the stream start is group
+// 0's, and the position after the last expected EOB is gstart[ngroups]
+__global__ __launch_bounds__(256) void sym_locate_kernel(const uint32_t* __restrict__ mask,
+                                                         const int64_t* __restrict__ tile_first,
+                                                         int64_t ntiles, int C, int w, int gpr,
+                                                         int64_t nbp_total, int64_t* gstart) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwv = (int64_t)gridDim.x * 4;
+  if (blockIdx.x == 0 && threadIdx.x == 0) gstart[0] = 0;
+  const int64_t D = (int64_t)C * w;                    // block-planes per block row
+  for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntiles; t += nwv) {
+    const uint64_t mk = (uint64_t)mask[t * 128 + 2 * lane] | ((uint64_t)mask[t * 128 + 2 * lane + 1] << 32);
+    const int cnt = __builtin_popcountll(mk);
+    const int incl = dec_wave_incl_sum(cnt);
+    int64_t e = tile_first[t] + (incl - cnt);           // EOB index of this lane's first EOB
+    uint64_t m = mk;
+    while (m) {
+      const int bit = __builtin_ctzll(m);
+      m &= m - 1;
+      const int64_t bpn = e + 1;                          // the block-plane after this EOB
+      ++e;
+      if (bpn > nbp_total) break;
+      const int64_t row = bpn / D, rem = bpn - row * D;
+      if (rem % (8 * C) == 0) gstart[row * gpr + rem / (8 * C)] = t * 4096 + lane * 64 + bit + 1;
+    }
   }
 }
 
@@ -241,7 +411,7 @@ hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, in
 // [F][h][w][C][64] int32 -> [F][H][W][3] float64 image (+ ycbcr2rgb)
 hipError_t launch_intra_decode_image(const int32_t* q, int64_t nframes, int64_t H, int64_t W,
                                      int C, const QTab& t, int unzigzag, int to_rgb, double* out,
-                                     hipStream_t s) {
+                                     hipStream_t s, const int* skip) {
   if (nframes <= 0 || H <= 0 || W <= 0) return hipSuccess;
   if ((C != 1 && C != 3) || H % 8 || W % 8) return hipErrorInvalidValue;
   DecArgs a{};
@@ -252,6 +422,7 @@ hipError_t launch_intra_decode_image(const int32_t* q, int64_t nframes, int64_t 
   a.nblk = nframes * (H / 8) * a.w;
   a.ngroups = nframes * (H / 8) * a.gpr;
   a.W3 = W * 3;
+  a.skip = skip;
 #define DEC_IMG(CC, ZZ)                                                        \
   return to_rgb ? launch_dec<CC, ZZ, DEC_IMAGE, true>(a, t, s)                 \
                 : launch_dec<CC, ZZ, DEC_IMAGE, false>(a, t, s)
@@ -261,6 +432,38 @@ hipError_t launch_intra_decode_image(const int32_t* q, int64_t nframes, int64_t 
     if (unzigzag) { DEC_IMG(3, true); } else { DEC_IMG(3, false); }
   }
 #undef DEC_IMG
+}
+
+// symbols -> image, fused: gstart from the EOB mask, then the group kernel (see above)
+hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const uint32_t* eobmask,
+                            const int64_t* tile_first, int64_t ntiles, int64_t nframes, int64_t H,
+                            int64_t W, int C, const QTab& t, int to_rgb, double* out,
+                            int64_t* gstart, int* fail, hipStream_t s) {
+  DecArgs a{};
+  a.out = out;
+  a.w = (int)(W / 8);
+  a.gpr = (a.w + 7) / 8;
+  a.nblk = nframes * (H / 8) * a.w;
+  a.ngroups = nframes * (H / 8) * a.gpr;
+  a.W3 = W * 3;
+  hipError_t e = hipMemsetAsync(gstart, 0xff, (size_t)(a.ngroups + 1) * 8, s);
+  if (e != hipSuccess) return e;
+  {
+    const int64_t nb = (ntiles + 3) / 4;
+    sym_locate_kernel<<<(unsigned)(nb < 256 * 16 ? (nb > 0 ? nb : 1) : 256 * 16), 256, 0, s>>>(
+        eobmask, tile_first, ntiles, C, a.w, a.gpr, (int64_t)C * a.nblk, gstart);
+  }
+  SymImageArgs z{sym, n, eob, gstart, fail};
+  auto go = [&](auto k) {
+    const unsigned grid = resident_grid_ptr(reinterpret_cast<const void*>(k), (a.ngroups + 3) / 4);
+    k<<<grid, 256, 0, s>>>(a, z, t);
+  };
+  if (C == 3) {
+    if (to_rgb) go(sym_image_kernel<3, true>); else go(sym_image_kernel<3, false>);
+  } else {
+    if (to_rgb) go(sym_image_kernel<1, true>); else go(sym_image_kernel<1, false>);
+  }
+  return hipGetLastError();
 }
 
 }  // namespace ivc

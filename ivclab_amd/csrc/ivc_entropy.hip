@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "ivc_internal.h"
 
 namespace ivc {
@@ -715,9 +717,11 @@ struct BothSinks {
 // trip), so errors and their messages are the general decoder's.
 constexpr int ZF_TILE = 4096, ZF_HALO = 128;
 
+// (eobmask, optional: bit i of word t * 128 + i / 32 = symbol t * ZF_TILE + i is an EOB slot —
+// the symbols -> image path locates its groups from it)
 __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict__ s, int64_t n,
                                                        int32_t eob, int32_t* __restrict__ tile_eobs,
-                                                       int* fail) {
+                                                       int* fail, uint32_t* __restrict__ eobmask) {
   __shared__ int red[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t ntiles = (n + ZF_TILE - 1) / ZF_TILE;
@@ -737,13 +741,24 @@ __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict
         for (int e = 0; e < 4; ++e) v[e] = i + e < n ? s[i + e] : 1;
       }
       int pv = i > 0 && i < n ? s[i - 1] : 1;       // the stream's first slot is a value slot
+      uint32_t bits = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         if (i + e < n) {
-          cnt += (v[e] == eob && pv != 0) ? 1 : 0;
+          const bool eb = v[e] == eob && pv != 0;
+          cnt += eb ? 1 : 0;
+          bits |= eb ? 1u << e : 0u;
           bad |= pv == 0 && v[e] <= 0;
         }
         pv = v[e];
+      }
+      if (eobmask) {
+        // 8 lanes' nibbles make one word: OR by DPP (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror)
+        bits <<= 4 * (tid & 7);
+        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);
+        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xf, 0xf, false);
+        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x141, 0xf, 0xf, false);
+        if ((tid & 7) == 0) eobmask[t * (ZF_TILE / 32) + (k * 256 + tid) / 8] = bits;
       }
     }
 #pragma unroll
@@ -913,9 +928,11 @@ struct ZrDecScratch {
   int64_t* tile_first;      // ntf + 1
   int64_t* fagg;
   int* flags;               // [0] fail, [1] ok
+  uint32_t* eobmask;        // symbols -> image: ntf * ZF_TILE / 32 words
+  int64_t* gstart;          // symbols -> image: ngroups + 1
 };
 int64_t align16(int64_t b) { return (b + 15) / 16 * 16; }
-ZrDecScratch zr_dec_scratch(void* scratch, int64_t n, int64_t* bytes) {
+ZrDecScratch zr_dec_scratch(void* scratch, int64_t n, int64_t* bytes, int64_t ngroups = -1) {
   const int64_t nt = scan_scratch_elems(n);
   const int64_t ntf = (n + ZF_TILE - 1) / ZF_TILE;
   uint8_t* b = (uint8_t*)scratch;
@@ -930,6 +947,12 @@ ZrDecScratch zr_dec_scratch(void* scratch, int64_t n, int64_t* bytes) {
   z.tile_first = (int64_t*)(b + o); o += align16((ntf + 1) * 8);
   z.fagg = (int64_t*)(b + o); o += align16(scan_scratch_elems(ntf) * 8);
   z.flags = (int*)(b + o); o += 16;
+  z.eobmask = nullptr;
+  z.gstart = nullptr;
+  if (ngroups >= 0) {
+    z.eobmask = (uint32_t*)(b + o); o += align16(ntf * (ZF_TILE / 32) * 4);
+    z.gstart = (int64_t*)(b + o); o += align16((ngroups + 1) * 8);
+  }
   if (bytes) *bytes = o;
   return z;
 }
@@ -941,6 +964,10 @@ int64_t zr_decode_scratch_bytes(int64_t n) {
   return bytes;
 }
 
+static hipError_t zr_decode_general(const ZrDecScratch& z, const int32_t* sym, int64_t n,
+                                    int64_t expected, int B, int32_t eob, int32_t* out,
+                                    int64_t* err, const int* skip, hipStream_t s);
+
 hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected, int B,
                                  int32_t eob, int32_t* out, void* scratch, int64_t* err,
                                  hipStream_t s) {
@@ -951,7 +978,7 @@ hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected
     const int64_t ntf = (n + ZF_TILE - 1) / ZF_TILE;
     const unsigned grid = (unsigned)(ntf < 256 * 8 ? ntf : 256 * 8);
     if ((e = hipMemsetAsync(z.flags, 0, 16, s)) != hipSuccess) return e;
-    zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags);
+    zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags, nullptr);
     e = device_scan<int64_t>(ntf, CountGen{z.tile_eobs}, SumI64{}, OffsetSink{z.tile_first, ntf},
                              z.fagg, s);
     if (e != hipSuccess) return e;
@@ -959,7 +986,14 @@ hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected
     zf_finish<<<1, 1, 0, s>>>(z.flags, z.tile_first + ntf, expected, z.flags + 1, err);
     skip = z.flags + 1;
   }
-  // the general decoder (every stream; skipped on the device when the fast one stood)
+  return zr_decode_general(z, sym, n, expected, B, eob, out, err, skip, s);
+}
+
+// the general decoder (every stream; skipped on the device when the fast one stood)
+static hipError_t zr_decode_general(const ZrDecScratch& z, const int32_t* sym, int64_t n,
+                                    int64_t expected, int B, int32_t eob, int32_t* out,
+                                    int64_t* err, const int* skip, hipStream_t s) {
+  hipError_t e;
   if ((e = hipMemsetAsync(z.ovf, 0xff, sizeof(unsigned long long), s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(z.total, 0, sizeof(ZrState), s)) != hipSuccess) return e;
   const int64_t nz = expected * B;
@@ -978,6 +1012,50 @@ hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected
   }
   zr_decode_verdict_gated<<<1, 1, 0, s>>>(sym, z.is_rl, n, expected, eob, z.total, z.ovf, err, skip);
   return hipGetLastError();
+}
+
+// IntraCodec.symbols2image on the device (intracodec.py:84-146): a well-formed stream goes
+// through the fused symbols -> image kernel (ivc_decode.hip: the coefficients stay in LDS);
+// otherwise — decided on the device — the general zero-run decoder fills `coef` and the
+// coefficient -> image kernel runs, so errors are the general decoder's.
+int64_t sym_image_scratch_bytes(int64_t n, int64_t ngroups) {
+  int64_t bytes = 0;
+  (void)zr_dec_scratch(nullptr, n, &bytes, ngroups);
+  return bytes;
+}
+
+hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, int64_t H,
+                                int64_t W, int C, const QTab& t, int32_t eob, int to_rgb,
+                                double* out, int32_t* coef, void* scratch, int64_t* err,
+                                hipStream_t s) {
+  const int64_t w = W / 8, gpr = (w + 7) / 8;
+  const int64_t ngroups = nframes * (H / 8) * gpr;
+  const int64_t expected = nframes * (H / 8) * w * C;     // block-planes
+  const ZrDecScratch z = zr_dec_scratch(scratch, n, nullptr, ngroups);
+  hipError_t e;
+  const int* skip = nullptr;
+  if (n > 0 && expected > 0 && eob != 0 && ((uintptr_t)sym & 15) == 0) {
+    const int64_t ntf = (n + ZF_TILE - 1) / ZF_TILE;
+    const unsigned grid = (unsigned)(ntf < 256 * 8 ? ntf : 256 * 8);
+    if ((e = hipMemsetAsync(z.flags, 0, 16, s)) != hipSuccess) return e;
+    zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags, z.eobmask);
+    e = device_scan<int64_t>(ntf, CountGen{z.tile_eobs}, SumI64{}, OffsetSink{z.tile_first, ntf},
+                             z.fagg, s);
+    if (e != hipSuccess) return e;
+    e = launch_sym_image(sym, n, eob, z.eobmask, z.tile_first, ntf, nframes, H, W, C, t, to_rgb,
+                         out, z.gstart, z.flags, s);
+    if (e != hipSuccess) return e;
+    zf_finish<<<1, 1, 0, s>>>(z.flags, z.tile_first + ntf, expected, z.flags + 1, err);
+    skip = z.flags + 1;
+  }
+  // (IVC_S2I_NO_FALLBACK=1, a test hook: the fused kernel's image stands alone, so a test can
+  // tell that it — not the general path — produced the image)
+  const char* nf = getenv("IVC_S2I_NO_FALLBACK");
+  const bool no_fallback = nf && nf[0] == '1';
+  if (skip && no_fallback) return hipSuccess;
+  e = zr_decode_general(z, sym, n, expected, 64, eob, coef, err, skip, s);
+  if (e != hipSuccess) return e;
+  return launch_intra_decode_image(coef, nframes, H, W, C, t, 1, to_rgb, out, s, skip);
 }
 
 // ---------------------------------------------------------------- symbol range --------

@@ -44,7 +44,18 @@ hipError_t launch_intra_decode(const int32_t* q, int64_t nblk, const QTab& t, in
                                double* out, hipStream_t s);
 hipError_t launch_intra_decode_image(const int32_t* q, int64_t nframes, int64_t H, int64_t W,
                                      int C, const QTab& t, int unzigzag, int to_rgb, double* out,
-                                     hipStream_t s);
+                                     hipStream_t s, const int* skip = nullptr);
+// fused zero-run symbols -> image (ivc_decode.hip) and its driver with the general fallback
+// (ivc_entropy.hip)
+hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const uint32_t* eobmask,
+                            const int64_t* tile_first, int64_t ntiles, int64_t nframes, int64_t H,
+                            int64_t W, int C, const QTab& t, int to_rgb, double* out,
+                            int64_t* gstart, int* fail, hipStream_t s);
+int64_t sym_image_scratch_bytes(int64_t n, int64_t ngroups);
+hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, int64_t H,
+                                int64_t W, int C, const QTab& t, int32_t eob, int to_rgb,
+                                double* out, int32_t* coef, void* scratch, int64_t* err,
+                                hipStream_t s);
 // store pacing of the fused coefficient kernels (ivc_kernels.hip): target total HBM GB/s, 0 = off
 double store_pace_gbps();
 double store_pace_late_fraction();

@@ -316,7 +316,7 @@ struct FusedArgs {
   int32_t* zr_out;
   int64_t zr_cap;
   int32_t zr_eob;
-  // OUT_SYMBOLS, optional: the clamped histogram of the emitted stream accumulated onto
+  // OUT_SYMH (OUT_SYMBOLS + histogram): the clamped histogram of the emitted stream added onto
   // zr_hist[clamp(v - zr_hist_lo, 0, zr_hist_n - 1)] (int64 counts), so the Huffman-table
   // exchange needs no pass over the stream
   unsigned long long* zr_hist;
@@ -607,7 +607,8 @@ __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* o
 // per-group counts (OUT_COUNT) or the symbol stream at scanned offsets (OUT_SYMBOLS).
 // OUT_LUMA: the luma-table plane only ([F][h][w][64], 4 B/px out instead of the reference's
 // 12 B/px 3-plane broadcast) — a reported variant, not the reference's output.
-enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2, OUT_LUMA = 3 };
+// OUT_SYMH: OUT_SYMBOLS plus the stream's histogram (FusedArgs::zr_hist).
+enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2, OUT_LUMA = 3, OUT_SYMH = 4 };
 
 // Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging.
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
@@ -721,24 +722,74 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
 // consecutive dword stores.
 constexpr int ZR_WIN = XS_PITCH * 8 * 8 / 4;   // int32 symbols in a wave's transpose region
 
-#ifndef IVC_ZR_EMIT2
-#define IVC_ZR_EMIT2 1
-#endif
-// OUT_SYMBOLS, one block-plane at a time with lane i = zig-zag position i: the plane's
-// nonzero mask is one ballot, its run starts and symbol count scalar bit operations, each
-// lane's slot two mbcnt; a lane writes its value (or a run's 0 and its length) into the
+// Staging address of raster coefficient j inside a block-plane for the emission pass (the
+// count pass and OUT_COEFS stage in zig-zag order).  Zig-zag staging makes the quantiser's
+// writes 2-3-way bank conflicted (lane (b, r) writes zig-zag position zz(8i + r) of block b:
+// 48 conflict cycles per group); this swizzle keeps both access patterns conflict-free:
+//  * writes: for each raster row i the 8 addresses are distinct mod 8, so with the block pitch
+//    (136 or 200, both = 8 mod 32) the 32 lanes of a ds_write_b32 lane group hit 32 banks;
+//  * reads: lane k of the emission pass reads zig-zag position k, and each half (k < 32,
+//    k >= 32) maps to 32 distinct banks.
+// Found by a randomised search; the properties are checked at compile time below.
+constexpr int c_sym_stage_h[64] = {
+    7,  6,  0,  1,  3,  5,  4,  2,  10, 14, 13, 11, 8,  15, 9,  36, 19, 17, 16, 18, 12, 21,
+    38, 39, 25, 26, 22, 27, 20, 32, 47, 37, 23, 24, 29, 35, 44, 33, 34, 46, 28, 30, 43, 45,
+    41, 40, 55, 42, 31, 50, 53, 48, 51, 54, 49, 52, 60, 56, 63, 62, 57, 61, 59, 58};
+constexpr int c_zz_order_h[64] = IVC_ZZ_ORDER;
+constexpr bool sym_stage_ok() {
+  bool used[64] = {};
+  for (int j = 0; j < 64; ++j) {
+    if (c_sym_stage_h[j] < 0 || c_sym_stage_h[j] >= 64 || used[c_sym_stage_h[j]]) return false;
+    used[c_sym_stage_h[j]] = true;
+  }
+  for (int i = 0; i < 8; ++i) {                      // write rows: distinct mod 8
+    int seen = 0;
+    for (int r = 0; r < 8; ++r) seen |= 1 << (c_sym_stage_h[8 * i + r] & 7);
+    if (seen != 0xff) return false;
+  }
+  for (int h = 0; h < 2; ++h) {                      // read halves: distinct mod 32
+    unsigned long long seen = 0;
+    for (int j = 0; j < 64; ++j)
+      if ((c_zz_order_h[j] >> 5) == h) seen |= 1ull << (c_sym_stage_h[j] & 31);
+    if (seen != 0xffffffffull) return false;
+  }
+  return true;
+}
+static_assert(sym_stage_ok(), "emission staging swizzle must be a conflict-free bijection");
+// the staging address the emission pass reads for zig-zag position k (lane k)
+__device__ __forceinline__ int sym_read_addr(int k) {
+  int a = 0;
+#pragma unroll
+  for (int j = 0; j < 64; ++j)
+    if (c_zz_order_h[j] == k) a = c_sym_stage_h[j];
+  return a;
+}
+
+// OUT_SYMBOLS / OUT_SYMH, one block-plane at a time with lane i = zig-zag position i: the
+// plane's nonzero mask is one ballot, its run starts and symbol count scalar bit operations,
+// each lane's slot two mbcnt; a lane writes its value (or a run's 0 and its length) into the
 // wave's LDS window (its last 64 words are the lanes' dummy slots), which is flushed to the
 // stream with consecutive-address stores before a block-plane that might not fit.  Per
 // group: two ds_write per block-plane instead of one per (plane, coefficient) slot and
-// window pass (the per-lane form below): 11.6 vs 13.3 ms for 256 x 4K (same-process A/B).
-// The stream's histogram rides along (a.zr_hist): each block-plane's nonzero values and run
-// lengths go to the workgroup's LDS bins (values in [-ZH_HALF, ZH_HALF); others straight to the
-// global histogram), its runs' 0 symbols and its EOB to two per-wave counters; the kernel adds
-// the bins and counters to the global histogram at its end.
+// window pass: 11.6 vs 13.3 ms for 256 x 4K (same-process A/B, r02).
+// OUT_SYMH also accumulates the stream's histogram (a.zr_hist) where the symbols leave: the
+// flush that copies the window to the stream adds each symbol to the workgroup's LDS bins, so
+// every symbol (values, run lengths, runs' 0s, EOBs, plane 2's repeat of plane 1) is counted
+// once with a few VALU per 64 symbols.  The hot symbols (-8..7 and the EOB) have 32 copies of
+// their bin, lane l adding to copy l % 32 — the copies of one value lie in 32 consecutive
+// words, so a ds_add_u32 of 32 lanes hits 32 banks whatever the values; values in
+// [-ZH_HALF, ZH_HALF) have one bin; the rest (rare) go to the global histogram behind one
+// wave-uniform test per flush iteration.  (r03 measured two earlier forms: a branch per
+// block-plane around the LDS atomic — ~13 scalar instructions each on the co-critical scalar
+// unit, emission 4.9 -> 8.0 ms — and a branch-free per-block-plane add — ~8 VALU per
+// block-plane, 7.66 ms.)
 constexpr int ZH_HALF = 512, ZH_BINS = 2 * ZH_HALF;
+constexpr int ZH_HOT_LO = -8, ZH_HOT_N = 17;            // -8..7, and the EOB as hot value 16
+constexpr int ZH_HOT = ZH_BINS;                           // 32 copies per hot value
+constexpr int ZH_TRASH = ZH_HOT + 32 * ZH_HOT_N;          // out-of-range values (uncounted)
+constexpr int ZH_LDS = ZH_TRASH + 1;
 struct ZrHistAcc {
-  uint32_t* bins;      // workgroup LDS bins (nullptr: no histogram)
-  uint32_t runs, eobs; // wave-uniform counts of the 0 symbols of runs and of EOBs
+  uint32_t* bins;      // workgroup LDS bins (OUT_SYMH)
 };
 __device__ __forceinline__ void zr_hist_global(const FusedArgs& a, int64_t v, uint32_t w) {
   int64_t k = v - a.zr_hist_lo;
@@ -747,17 +798,18 @@ __device__ __forceinline__ void zr_hist_global(const FusedArgs& a, int64_t v, ui
                          __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int C, bool DUP>
+template <int C, bool DUP, bool HIST>
 __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, int nb,
                                               int64_t gbase, ZrHistAcc& H) {
   constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging
   constexpr int PITCH = os_pitch<C, DUP>();
   const int lane = threadIdx.x & 63;
+  const int ra = sym_read_addr(lane);           // zig-zag position `lane` in the swizzled staging
   int32_t xv[8][NP];
 #pragma unroll
   for (int b = 0; b < 8; ++b)
 #pragma unroll
-    for (int p = 0; p < NP; ++p) xv[b][p] = os[b * PITCH + p * 64 + lane];
+    for (int p = 0; p < NP; ++p) xv[b][p] = os[b * PITCH + p * 64 + ra];
   __builtin_amdgcn_wave_barrier();              // staging read: the region becomes the window
   int32_t* zs = os;
   int64_t base = gbase;
@@ -767,8 +819,21 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
   auto flush = [&]() {
     __builtin_amdgcn_wave_barrier();
     const int64_t lim = a.zr_cap - base;
-    for (int j = lane; j < fill; j += 64)
-      if (j < lim) a.zr_out[base + j] = zs[j];
+    for (int j = lane; j < fill; j += 64) {
+      const int32_t v = zs[j];
+      if (j < lim) a.zr_out[base + j] = v;
+      if constexpr (HIST) {
+        const uint32_t h0 = (uint32_t)(v - ZH_HOT_LO);             // -8..7 -> 0..15
+        const uint32_t hv = v == a.zr_eob ? 16u : (h0 < 16u ? h0 : (uint32_t)ZH_HOT_N);
+        const uint32_t k = (uint32_t)(v + ZH_HALF);
+        const uint32_t kb = hv < (uint32_t)ZH_HOT_N ? ZH_HOT + 32 * hv + (lane & 31)
+                                                    : (k < (uint32_t)ZH_BINS ? k : (uint32_t)ZH_TRASH);
+        atomicAdd(H.bins + kb, 1u);
+        if (__builtin_expect(__ballot(kb == (uint32_t)ZH_TRASH) != 0, 0)) {
+          if (kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v, 1u);
+        }
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     base += fill;
     fill = 0;
@@ -804,20 +869,6 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
       w1[p] = nz || rs || lane == last1;
       v1[p] = nz || rs ? x : a.zr_eob;                      // x == 0 at a run start
       v2[p] = rs ? __builtin_ctzll(m >> lane) : a.zr_eob;
-      if (H.bins) {
-        // the block-plane's symbols besides its runs' 0s and its EOB: the nonzero values and
-        // the run lengths (plane 1 counts twice when plane 2 repeats it)
-        const uint32_t wgt = p == 1 ? R1 : 1;
-        H.runs += wgt * (uint32_t)__builtin_popcountll(st);
-        H.eobs += wgt;
-        if (nz || rs) {
-          const int u = nz ? x : v2[p];
-          if ((unsigned)(u + ZH_HALF) < (unsigned)ZH_BINS)
-            atomicAdd(H.bins + (u + ZH_HALF), wgt);
-          else
-            zr_hist_global(a, u, wgt);
-        }
-      }
     }
     // one window check per block (its <= 3 x 97 symbols always fit an empty window)
     int tb = 0;
@@ -844,29 +895,29 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
   flush();
 }
 
+// OUT_COUNT: the group's symbol count from the zig-zag staging.  Lane (b, r) takes zig-zag
+// positions 8r .. 8r+7 of block b; a block's nonzero mask is the OR of its 8 lanes' bytes.
 template <int C, bool DUP, int OUTM>
 __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b, int r, int nb,
                                          int64_t gid, ZrHistAcc& H) {
-  if constexpr (OUTM == OUT_SYMBOLS && IVC_ZR_EMIT2) {
-    zr_group_emit<C, DUP>(a, os, nb, a.zr_off[gid], H);
+  if constexpr (OUTM == OUT_SYMBOLS || OUTM == OUT_SYMH) {
+    zr_group_emit<C, DUP, OUTM == OUT_SYMH>(a, os, nb, a.zr_off[gid], H);
     return;
   }
   constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging
   constexpr int PITCH = os_pitch<C, DUP>();
   const bool live = b < nb;
   const int lane = threadIdx.x & 63;
-  int32_t val[NP][8];
   uint64_t m[NP], st[NP];
   int cnt[NP];
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     const int4* src = reinterpret_cast<const int4*>(os + b * PITCH + p * 64 + 8 * r);
     const int4 v0 = src[0], v1 = src[1];
-    val[p][0] = v0.x; val[p][1] = v0.y; val[p][2] = v0.z; val[p][3] = v0.w;
-    val[p][4] = v1.x; val[p][5] = v1.y; val[p][6] = v1.z; val[p][7] = v1.w;
+    const int32_t val[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
     uint32_t byte = 0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) byte |= (uint32_t)(val[p][k] != 0) << k;
+    for (int k = 0; k < 8; ++k) byte |= (uint32_t)(val[k] != 0) << k;
     // OR over the block's 8 lanes by DPP (quad_perm 1,0,3,2; 2,3,0,1; row_half_mirror):
     // VALU only, no LDS round trips
     uint32_t lo = live && r < 4 ? byte << (8 * r) : 0u;
@@ -886,71 +937,11 @@ __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b,
     cnt[p] = live ? __builtin_popcountll(lm) + 2 * __builtin_popcountll(st[p]) + 1 : 0;
   }
   __builtin_amdgcn_wave_barrier();                            // staging read: region free
-  const int c2 = cnt[NP - 1];
-  const int tb = cnt[0] + cnt[1] + c2;                       // the block's symbols
-  if constexpr (OUTM == OUT_COUNT) {
-    int v = 0;                                                // lane 8b holds block b's total
+  const int tb = cnt[0] + cnt[1] + cnt[NP - 1];               // the block's symbols
+  int v = 0;                                                  // lane 8b holds block b's total
 #pragma unroll
-    for (int bb = 0; bb < 8; ++bb) v += __builtin_amdgcn_readlane(tb, 8 * bb);
-    if (lane == 0) a.zr_counts[gid] = v;
-  } else {
-    // exclusive prefix of the block totals over b (lane groups of 8)
-    int inc = tb;
-#pragma unroll
-    for (int d = 8; d < 64; d <<= 1) {
-      const int o = __shfl_up(inc, d);
-      if (lane >= d) inc += o;
-    }
-    const int pre = inc - tb;                                 // symbols of blocks before b
-    const int gtot = __shfl(inc, 56);                         // the group's symbols
-    const int64_t gbase = a.zr_off[gid];
-    // each lane's first slot per plane: symbols of the block's zig-zag positions < 8r
-    const uint64_t low = r == 0 ? 0ull : (~0ull >> (64 - 8 * r));
-    int first[3];
-    {
-      int pb = pre;
-#pragma unroll
-      for (int pp = 0; pp < 3; ++pp) {
-        const int p = pp < NP ? pp : NP - 1;
-        first[pp] = pb + __builtin_popcountll(m[p] & low) + 2 * __builtin_popcountll(st[p] & low);
-        pb += cnt[p];
-      }
-    }
-    int32_t* zs = os;                                         // staging consumed above
-    for (int w0 = 0; w0 < gtot; w0 += ZR_WIN) {
-      auto put = [&](int pos, int32_t v) {
-        const unsigned o = (unsigned)(pos - w0);
-        if (o < (unsigned)ZR_WIN) zs[o] = v;
-      };
-      if (live) {
-#pragma unroll
-        for (int pp = 0; pp < 3; ++pp) {
-          const int p = pp < NP ? pp : NP - 1;
-          const uint32_t mb = (uint32_t)(m[p] >> (8 * r)) & 0xffu;
-          const uint32_t sb = (uint32_t)(st[p] >> (8 * r)) & 0xffu;
-          int pos = first[pp];
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            if ((mb >> k) & 1u) {
-              put(pos, val[p][k]);
-              pos += 1;
-            } else if ((sb >> k) & 1u) {
-              put(pos, 0);
-              put(pos + 1, __builtin_ctzll(m[p] >> (8 * r + k)));
-              pos += 2;
-            }
-          }
-          if (r == 0) put(first[pp] + cnt[p] - 1, a.zr_eob);     // r = 0: first = plane start
-        }
-      }
-      __builtin_amdgcn_wave_barrier();
-      const int n = gtot - w0 < ZR_WIN ? gtot - w0 : ZR_WIN;
-      const int64_t dst = gbase + w0;
-      for (int j = lane; j < n; j += 64)
-        if (dst + j < a.zr_cap) a.zr_out[dst + j] = zs[j];
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
+  for (int bb = 0; bb < 8; ++bb) v += __builtin_amdgcn_readlane(tb, 8 * bb);
+  if (lane == 0) a.zr_counts[gid] = v;
 }
 
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
@@ -960,11 +951,12 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
                 "symbols need zig-zag order");
   static_assert(OUTM != OUT_LUMA || C == 1, "the luma-only output is for C = 1 images");
   constexpr bool COEF = OUTM == OUT_COEFS || OUTM == OUT_LUMA;
+  constexpr bool SYM = OUTM == OUT_SYMBOLS || OUTM == OUT_SYMH;   // emission pass
   typedef WaveLds<T, C, DUP> L;
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
   __shared__ double srq[FAST ? 192 : 1];
   __shared__ D sq[192];
-  __shared__ uint32_t zh[OUTM == OUT_SYMBOLS ? ZH_BINS : 1];
+  __shared__ uint32_t zh[OUTM == OUT_SYMH ? ZH_LDS : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   const int b = lane >> 3, r = lane & 7;
@@ -975,18 +967,22 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
     if constexpr (FAST) srq[i] = (dct2_scale((i >> 3) & 7) * dct2_scale(i & 7)) * (1.0 / t.q[i]);
   }
   // zig-zag positions of this lane's column (raster i*8 + r), packed 4 per register
+  // (the emission pass stages through the bank-conflict-free swizzle instead)
   uint32_t zp0 = 0, zp1 = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    zp0 |= (uint32_t)(ZZ ? c_zz_order[i * 8 + r] : i * 8 + r) << (8 * i);
-    zp1 |= (uint32_t)(ZZ ? c_zz_order[(i + 4) * 8 + r] : (i + 4) * 8 + r) << (8 * i);
-  }
-  ZrHistAcc hacc{nullptr, 0u, 0u};
-  if constexpr (OUTM == OUT_SYMBOLS) {
-    if (a.zr_hist) {
-      for (int i = tid; i < ZH_BINS; i += 256) zh[i] = 0;
-      hacc.bins = zh;
+    if constexpr (SYM) {
+      zp0 |= (uint32_t)c_sym_stage_h[i * 8 + r] << (8 * i);
+      zp1 |= (uint32_t)c_sym_stage_h[(i + 4) * 8 + r] << (8 * i);
+    } else {
+      zp0 |= (uint32_t)(ZZ ? c_zz_order[i * 8 + r] : i * 8 + r) << (8 * i);
+      zp1 |= (uint32_t)(ZZ ? c_zz_order[(i + 4) * 8 + r] : (i + 4) * 8 + r) << (8 * i);
     }
+  }
+  ZrHistAcc hacc{nullptr};
+  if constexpr (OUTM == OUT_SYMH) {
+    for (int i = tid; i < ZH_LDS; i += 256) zh[i] = 0;
+    hacc.bins = zh;
   }
   __syncthreads();  // tables only; the loop below never synchronises across waves (but the
                     // symbol histogram's bins are flushed after a barrier at the end)
@@ -1134,14 +1130,19 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if constexpr (OUTM == OUT_SYMBOLS) {
-    if (a.zr_hist) {
-      __syncthreads();
-      for (int i = tid; i < ZH_BINS; i += 256)
-        if (zh[i]) zr_hist_global(a, i - ZH_HALF, zh[i]);
-      if (lane == 0) {
-        if (hacc.runs) zr_hist_global(a, 0, hacc.runs);
-        if (hacc.eobs) zr_hist_global(a, a.zr_eob, hacc.eobs);
+  if constexpr (OUTM == OUT_SYMH) {
+    __syncthreads();
+    for (int i = tid; i < ZH_BINS; i += 256)
+      if (zh[i]) zr_hist_global(a, i - ZH_HALF, zh[i]);
+    for (int i0 = 0; i0 < ZH_HOT_N * 32; i0 += 256) {
+      // the 32 copies of a hot value are 32 consecutive lanes of one wave
+      const int i = i0 + tid;
+      uint32_t c = i < ZH_HOT_N * 32 ? zh[ZH_HOT + i] : 0u;
+#pragma unroll
+      for (int d = 16; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+      if ((i & 31) == 0 && i < ZH_HOT_N * 32 && c) {
+        const int hv = i >> 5;
+        zr_hist_global(a, hv == 16 ? (int64_t)a.zr_eob : (int64_t)(hv + ZH_HOT_LO), c);
       }
     }
   }
@@ -1713,7 +1714,8 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
   }
   if (e == hipSuccess) e = hipMemcpyAsync(nsym, off + ngroups, 8, hipMemcpyDeviceToDevice, s);
   if (e == hipSuccess && a.zr_cap > 0) {
-    launch_fused_zr<TI, C, DUP, CM, OUT_SYMBOLS>(a, t, s);
+    if (a.zr_hist) launch_fused_zr<TI, C, DUP, CM, OUT_SYMH>(a, t, s);
+    else launch_fused_zr<TI, C, DUP, CM, OUT_SYMBOLS>(a, t, s);
     e = hipGetLastError();
   }
   if (counts) (void)hipFreeAsync(counts, s);

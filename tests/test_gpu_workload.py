@@ -227,3 +227,42 @@ def test_chunked_inter_encode_with_side_stream_histograms():
     wmv, wq = c_inter_encode(host[3], host[4], sr, 1.0)
     assert_bits(mv2[3], wmv[..., 0], "mv pair 3")
     assert_bits(q2[3], wq.reshape(H // 8, W // 8, 3, 64), "q pair 3")
+
+
+@pytest.mark.parametrize("C", [3, 1])
+def test_symbols2image_fused_adversarial(monkeypatch, C):
+    """The fused symbols -> image kernel (ivc_decode.hip sym_image_kernel: zero-run expansion
+    into LDS, dequantise, IDCT, unpatch, ycbcr2rgb; intracodec.py:84-146 + zerorun.py:44-88)
+    alone — IVC_S2I_NO_FALLBACK=1 keeps the general decoder from overwriting its image — on
+    coefficients built to stress it: all-zero blocks (one EOB per block-plane, so 4096-symbol
+    tiles hold dozens of group starts), densest blocks (value, 0, run 1, ... = 97 symbols per
+    block-plane), long runs, a value at zig-zag position 63, large DCs, a ragged last group
+    (w = 125 block columns) and a stream of 130k-380k symbols over 30-90 tiles; against the
+    oracle chain (ZeroRunCoder.decode, unflatten, dequantise, IDCT, unpatch, ycbcr2rgb)."""
+    monkeypatch.setenv("IVC_S2I_NO_FALLBACK", "1")
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(40 + C)
+    F, H, W = 2, 128, 1000
+    h, w = H // 8, W // 8
+    q = rng.integers(-3, 4, (F, h, w, C, 64)).astype(np.int32)
+    q[..., 8:] *= rng.random(q[..., 8:].shape) < 0.15
+    kind = rng.integers(0, 5, (F, h, w, C))
+    q[kind == 0] = 0                                              # all-zero block-planes
+    dense = np.where(np.arange(64) % 2 == 1, 5, 0).astype(np.int32)
+    q[kind == 1] = dense                                          # (0, 1, 5) x 32 + EOB = 97
+    q[kind == 2, 1:63] = 0                                        # one long run, then pos 63
+    q[kind == 2, 63] = -7
+    q[..., 0] = np.where(kind == 3, rng.integers(-1500, 1500, kind.shape), q[..., 0])
+    sym = np.asarray(O.zerorun_encode_fast(q.reshape(-1, 64)), dtype=np.int32)
+    assert sym.size > 120_000
+    table = PatchQuant(0.8).get_quantization_table()
+    out = torch.full((F, H, W, 3), float("nan"), dtype=torch.float64, device=dev)
+    err = torch.full((3,), -1, dtype=torch.int64, device=dev)
+    D.symbols2image(torch.from_numpy(sym).to(dev), C, table, out, err, to_rgb=(C == 3))
+    torch.cuda.synchronize()
+    assert err.tolist() == [0, 0, 0]
+    for f in range(F):
+        want = O.unpatch(O.intra_decode(q[f], 0.8, unzigzag=True))
+        if C == 3:
+            want = O.ycbcr2rgb(want)
+        assert_bits(out[f].cpu().numpy(), want, f"fused symbols2image C={C} frame {f}")

@@ -1,6 +1,6 @@
 """Same-process A/B timing of libivc variants (ab/*.so) on the symbol legs of bench.py: the
-zero-run encode of the cfg3 zig-zag coefficients, the fused pixels -> symbols path, the
-symbol histogram and min/max.  Every variant's outputs are compared with the first one's.
+zero-run encode of the cfg3 zig-zag coefficients, the fused pixels -> symbols path (without and with the
+emission pass's histogram), the symbol histogram and min/max.  Every variant's outputs are compared with the first one's.
     python tools/ab/ab_symbols.py ab/base.so ab/new.so [--frames 256] [--rounds 5]"""
 import argparse
 import ctypes
@@ -48,6 +48,7 @@ sym = torch.empty(nsym, dtype=torch.int32, device=dev)
 nsd = torch.zeros(1, dtype=torch.int64, device=dev)
 hist = torch.zeros(4200, dtype=torch.int64, device=dev)
 mm = torch.empty(2, dtype=torch.int32, device=dev)
+hist2 = torch.zeros(8194, dtype=torch.int64, device=dev)
 
 
 def timeit(fn, reps=3):
@@ -67,6 +68,9 @@ legs = {
     "intra_symbols": lambda L: N.check(L.ivc_intra_symbols_dev(
         img.data_ptr(), 1, F, H, W, 1, t.ctypes.data, 4000, sym.data_ptr(), nsym, nsd.data_ptr(),
         stream)),
+    "symbols_hist": lambda L: (hist2.zero_(), N.check(L.ivc_intra_symbols_hist_dev(
+        img.data_ptr(), 1, F, H, W, 1, t.ctypes.data, 4000, sym.data_ptr(), nsym, nsd.data_ptr(),
+        hist2.data_ptr(), -4097, 8194, stream))),
     "histogram": lambda L: (hist.zero_(), N.check(L.ivc_histogram_i32_dev(
         sym.data_ptr(), nsym, -64, 4200, hist.data_ptr(), stream))),
     "minmax": lambda L: N.check(L.ivc_minmax_i32_dev(sym.data_ptr(), nsym, mm.data_ptr(), stream)),
@@ -79,7 +83,8 @@ for rnd in range(args.rounds):
             res[(leg, n)].append(timeit(lambda: fn(L)))
             if rnd == 0:
                 torch.cuda.synchronize()
-                outs = {"zerorun_encode": sym, "intra_symbols": sym, "histogram": hist, "minmax": mm}
+                outs = {"zerorun_encode": sym, "intra_symbols": sym, "symbols_hist": hist2,
+                        "histogram": hist, "minmax": mm}
                 digest = (int(outs[leg].view(-1)[:1 << 24].to(torch.int64).sum().item()),
                           int(outs[leg].numel()))
                 check.setdefault(leg, digest)

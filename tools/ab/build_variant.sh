@@ -16,10 +16,6 @@ else
 fi
 mkdir -p "$ROOT/ab"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math \
-  "$@" -o "$ROOT/ab/$NAME.so" "$SRC"/ivclab_amd/csrc/ivc_kernels.hip "$SRC"/ivclab_amd/csrc/ivc_motion.hip \
-  $( [ -f "$SRC"/ivclab_amd/csrc/ivc_entropy.hip ] && echo "$SRC"/ivclab_amd/csrc/ivc_entropy.hip ) \
-  $( [ -f "$SRC"/ivclab_amd/csrc/ivc_color.hip ] && echo "$SRC"/ivclab_amd/csrc/ivc_color.hip ) \
-  $( [ -f "$SRC"/ivclab_amd/csrc/ivc_huffman.hip ] && echo "$SRC"/ivclab_amd/csrc/ivc_huffman.hip ) \
-  "$SRC"/ivclab_amd/csrc/ivc_capi.hip
+  "$@" -o "$ROOT/ab/$NAME.so" "$SRC"/ivclab_amd/csrc/*.hip
 rm -rf "$SRC"
 echo "built ab/$NAME.so"

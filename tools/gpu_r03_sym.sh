@@ -16,8 +16,8 @@ d = json.load(open("gpurun_out/sym.json"))
 print("image2symbols ms", d["image2symbols"]["ms"], "zerorun ms", d["zerorun"]["ms"],
       "exchange ms", d["exchange"]["ms"], "verify", d["verify"]["ok"])
 dc = d.get("decode", {})
-print("decode ms", dc.get("ms"), "kernel ms", dc.get("roofline", {}).get("kernel_ms"),
-      "frac", dc.get("roofline", {}).get("frac"), "zerorun_decode_ms", dc.get("zerorun_decode_ms"))
+print("decode ms", dc.get("ms"), "frac", dc.get("roofline", {}).get("frac"),
+      "coefficients_to_image ms", dc.get("coefficients_to_image", {}).get("kernel_ms"))
 PY
 if [ -n "$PROF" ]; then
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_sym" -o run -- python bench.py $SYM_ONLY --no-verify > gpurun_out/prof_sym.log 2>&1 || { tail -20 gpurun_out/prof_sym.log; exit 1; }

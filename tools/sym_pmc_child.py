@@ -1,6 +1,6 @@
 """Profiling child: the cfg3 entropy stages alone — ZeroRunCoder.encode of the zig-zag
 coefficients (zw_count / scan / zw_emit) and the fused pixels -> symbols path (fused encoder
-OUT_COUNT / scan / OUT_SYMBOLS), once each on 256 (SYM_FRAMES) 4K frames.  Run under
+OUT_COUNT / scan / OUT_SYMBOLS, then OUT_SYMH with the histogram), once each on 256 (SYM_FRAMES) 4K frames.  Run under
 `rocprofv3 --pmc ...`."""
 import os
 import sys
@@ -33,6 +33,9 @@ def main():
     D.zerorun_encode(out.view(nblk, 64), offs, sym)
     nsd = torch.zeros(1, dtype=torch.int64, device=dev)
     D.intra_symbols(frames, table, sym, nsd)
+    # the bench's form: the emission pass also accumulates the stream's histogram (OUT_SYMH)
+    hist = torch.zeros(bench.HIST_BINS + 2, dtype=torch.int64, device=dev)
+    D.intra_symbols(frames, table, sym, nsd, hist=hist, hist_lo=bench.HIST_LO - 1)
     torch.cuda.synchronize()
     print("sym_pmc_child done", nsym)
 
