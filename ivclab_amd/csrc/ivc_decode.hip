@@ -100,16 +100,16 @@ __device__ __forceinline__ void dec_load(const DecArgs& a, int64_t g, int lane, 
 // qs + (b * C + p) * DQ_PITCH, zig-zag or raster order inside) and its output: DEC_BLOCKS
 // [nblk][3][8][8] or DEC_IMAGE rows.  Shared by intra_decode_kernel (coefficients from HBM) and
 // sym_image_kernel (coefficients expanded from the zero-run stream).
-template <int C, int OUTL, bool RGB>
+template <int C, int OUTL, bool RGB, typename Q = int32_t, int QP = DQ_PITCH>
 __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup& G,
-                                               const int32_t* qs, double* xs, const double* tq,
+                                               const Q* qs, double* xs, const double* tq,
                                                const uint32_t* pos, int b, int r, int lane) {
   double o[RGB || OUTL == DEC_IMAGE ? 3 : 1][8];
   int32_t qv[8];
 #pragma unroll
   for (int p = 0; p < 3; ++p) {
     if (C == 3 || p == 0) {
-      const int32_t* qb = qs + (b * C + (C == 3 ? p : 0)) * DQ_PITCH;
+      const Q* qb = qs + (b * C + (C == 3 ? p : 0)) * QP;
 #pragma unroll
       for (int k = 0; k < 8; ++k) qv[k] = qb[(pos[k >> 2] >> (8 * (k & 3))) & 0xff];
     }
@@ -244,9 +244,9 @@ __global__ __launch_bounds__(256) void intra_decode_kernel(DecArgs a, QTab t) {
 // into the zeroed LDS staging of dec_group_math: lane j takes symbol j of the chunk; its slot
 // type follows from the previous symbol (a run-length slot iff it is 0), its coefficient count
 // (1 for a nonzero value, the run length for a 0, none for run-length and EOB slots) and its
-// EOB flag are prefix-summed across the wave in one packed DPP scan, and a DPP max-scan of the
-// EOB lanes' coefficient offsets gives each lane's block-plane start, so a nonzero value lands
-// at (its block-plane, offset - start).  Any violation (a block-plane past 64 coefficients, a
+// EOB flag are prefix-summed across the wave in one packed DPP scan, and each EOB lane records
+// in LDS the offset at which the next block-plane starts, so a nonzero value lands at (its
+// block-plane, offset - that block-plane's start).  Any violation (a block-plane past 64 coefficients, a
 // group whose EOB count or bounds do not match) sets `fail`, and the general path (zero-run
 // decode into coefficients + intra_decode_kernel, gated on the device) overwrites the image.
 // HBM per pixel: the stream's ~6.8 B (cfg3: 4 B/symbol) + 24 B of RGB float64.
@@ -259,17 +259,6 @@ __device__ __forceinline__ int dec_wave_incl_sum(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31
   return v;
 }
-// inclusive max-scan over the wave for v >= 0 (0 is the identity)
-__device__ __forceinline__ int dec_wave_incl_max(int v) {
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false));
-  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false));
-  return v;
-}
-
 struct SymImageArgs {
   const int32_t* sym;
   int64_t n;
@@ -278,11 +267,23 @@ struct SymImageArgs {
   int* fail;
 };
 
+// A group's symbols (854 on average for the cfg3 stream, at most 24 x 97) are staged into the
+// wave's LDS with all their 16-byte loads in flight at once — up to SYM_SEG symbols per round,
+// in the region the IDCT's transpose uses afterwards — and parsed from there (a first version
+// loaded 64 symbols per iteration, one HBM latency per chunk: 25 ms for the cfg3 stream).
+constexpr int SYM_SEG = 1280;                          // symbols staged per round (5 KB)
+// coefficients staged as int16 (a value outside int16 sends the stream to the general path):
+// half the LDS of int32 rows, 4 workgroups per CU instead of 3
+constexpr int SYM_QP = 72;                             // int16 per staged block-plane (144 B)
+constexpr int SYM_XW = SYM_SEG + 8;                    // int32 words: [3] = prev, [4 ..] symbols
+constexpr int SYM_XD = (SYM_XW / 2 > DX_WAVE ? SYM_XW / 2 : DX_WAVE);   // doubles per wave
+
 template <int C, bool RGB>
-__global__ __launch_bounds__(256) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t) {
-  constexpr int QS = 8 * C * DQ_PITCH;
-  __shared__ __attribute__((aligned(16))) int32_t qs_all[4 * QS];
-  __shared__ __attribute__((aligned(16))) double xs_all[4 * DX_WAVE];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t) {
+  constexpr int QS = 8 * C * SYM_QP;                   // int16 per wave
+  __shared__ __attribute__((aligned(16))) int16_t qs_all[4 * QS];
+  __shared__ int bps_all[4 * 32];                       // block-plane start offsets per wave
+  __shared__ __attribute__((aligned(16))) double xs_all[4 * SYM_XD];
   __shared__ double tq[192];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -292,38 +293,61 @@ __global__ __launch_bounds__(256) void sym_image_kernel(DecArgs a, SymImageArgs 
   dec_gather_pos<true>(r, pos);
   __syncthreads();   // the table only
 
-  int32_t* qs = qs_all + wave * QS;
-  double* xs = xs_all + wave * DX_WAVE;
+  int16_t* qs = qs_all + wave * QS;
+  int* bps = bps_all + wave * 32;
+  double* xs = xs_all + wave * SYM_XD;
+  int32_t* st = reinterpret_cast<int32_t*>(xs) + 4;    // st[-1]: the symbol before the round
   const int64_t nw = (int64_t)gridDim.x * 4;
   bool bad = false;
-  for (int64_t g = (int64_t)blockIdx.x * 4 + wave; g < a.ngroups; g += nw) {
+  // the group bounds are loaded one group ahead (scalar loads in flight during the group)
+  int64_t g = (int64_t)blockIdx.x * 4 + wave;
+  int64_t Sn = g < a.ngroups ? z.gstart[g] : 0, En = g < a.ngroups ? z.gstart[g + 1] : 0;
+  for (; g < a.ngroups; g += nw) {
     const DecGroup G = dec_group<DEC_IMAGE>(a, g);
-    const int64_t S = z.gstart[g], E = z.gstart[g + 1];
-    const int nbp = C * G.nb;                          // block-planes (EOBs) of the group
-    // zero the staging (C x 8 rows of DQ_PITCH int32)
-#pragma unroll
-    for (int j = 0; j < (QS / 4 + 63) / 64; ++j) {
-      const int c = j * 64 + lane;
-      if (c < QS / 4) *reinterpret_cast<dec_u32x4*>(qs + 4 * c) = dec_u32x4{0, 0, 0, 0};
+    const int64_t S = Sn, E = En;
+    if (g + nw < a.ngroups) {
+      Sn = z.gstart[g + nw];
+      En = z.gstart[g + nw + 1];
     }
-    __builtin_amdgcn_wave_barrier();
+    const int nbp = C * G.nb;                          // block-planes (EOBs) of the group
     if (S < 0 || E <= S || E > z.n || E - S > (int64_t)nbp * 130) {
       bad = true;                                      // wave-uniform
-    } else {
-      const int len = (int)(E - S);
-      const __amdgpu_buffer_rsrc_t rs = dec_rsrc(z.sym + S, (uint32_t)len * 4u);
-      int cur = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, lane * 4, 0, 0);
-      int prevc = 1;          // the symbol before the chunk (the group starts at a value slot)
-      int pcarry = 0;         // coefficients of the group before the chunk
-      int bpcarry = 0;        // EOBs before the chunk
-      int basecarry = 0;      // coefficient offset at which the current block-plane starts
-      for (int c0 = 0; c0 < len; c0 += 64) {
-        const int nxtv = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, (c0 + 64 + lane) * 4, 0, 0);
-        const int nxt0 = __builtin_amdgcn_readfirstlane(nxtv);
-        const int prv = __builtin_amdgcn_update_dpp(prevc, cur, 0x138, 0xf, 0xf, false);  // wave_shr:1
-        const int nx = __builtin_amdgcn_update_dpp(nxt0, cur, 0x130, 0xf, 0xf, false);    // wave_shl:1
-        const bool valid = c0 + lane < len;
-        const bool rl = prv == 0;                        // a run-length slot
+      continue;
+    }
+    const int len = (int)(E - S);
+    const __amdgpu_buffer_rsrc_t rs = dec_rsrc(z.sym + S, (uint32_t)len * 4u);
+    // zero the coefficient staging (C x 8 rows of SYM_QP int16)
+#pragma unroll
+    for (int j = 0; j < (QS / 8 + 63) / 64; ++j) {
+      const int c = j * 64 + lane;
+      if (c < QS / 8) *reinterpret_cast<dec_u32x4*>(qs + 8 * c) = dec_u32x4{0, 0, 0, 0};
+    }
+    if (lane == 0) bps[0] = 0;
+    int pcarry = 0;         // coefficients of the group before the chunk
+    int bpcarry = 0;        // EOBs before the chunk
+    int prevc = 1;          // the symbol before the round (a group starts at a value slot)
+    for (int s0 = 0; s0 < len; s0 += SYM_SEG) {
+      // one round: every load in flight, then the LDS writes
+      dec_u32x4 v[SYM_SEG / 256];
+#pragma unroll
+      for (int j = 0; j < SYM_SEG / 256; ++j)
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (s0 + j * 256 + lane * 4) * 4, 0, 0);
+      const int nxt = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, (s0 + SYM_SEG) * 4, 0, 0);
+      __builtin_amdgcn_wave_barrier();                 // the previous round's reads are done
+#pragma unroll
+      for (int j = 0; j < SYM_SEG / 256; ++j)
+        *reinterpret_cast<dec_u32x4*>(st + j * 256 + lane * 4) = v[j];
+      if (lane == 0) {
+        st[-1] = prevc;
+        st[SYM_SEG] = nxt;
+      }
+      __builtin_amdgcn_wave_barrier();
+      const int rlen = len - s0 < SYM_SEG ? len - s0 : SYM_SEG;
+      for (int c0 = 0; c0 < rlen; c0 += 64) {
+        const int i = c0 + lane;
+        const int cur = st[i], prv = st[i - 1], nx = st[i + 1];
+        const bool valid = i < rlen;
+        const bool rl = prv == 0;                      // a run-length slot
         const bool eobf = valid && !rl && cur == z.eob;
         const bool isval = valid && !rl && !eobf;
         const int run = nx < 1 ? 1 : (nx > 4095 ? 4095 : nx);
@@ -333,26 +357,26 @@ __global__ __launch_bounds__(256) void sym_image_kernel(DecArgs a, SymImageArgs 
         const int excl = incl - packed;
         const int pex = pcarry + (excl & 0xfffff);     // this slot's coefficient offset
         const int bp = bpcarry + (excl >> 20);          // its block-plane
-        const int mx = dec_wave_incl_max(eobf ? pex : 0);
-        int base = __builtin_amdgcn_update_dpp(0, mx, 0x138, 0xf, 0xf, false);  // exclusive
-        base = max(base, basecarry);
-        const int off = pex - base;                      // offset inside the block-plane
+        // block-plane starts through LDS: an EOB lane records where the next block-plane
+        // starts, then every lane reads its own block-plane's start (in-order LDS per wave)
+        const bool bpok = bp < nbp;
+        if (eobf && bpok) bps[bp + 1] = pex;
+        __builtin_amdgcn_wave_barrier();
+        const int off = pex - bps[bpok ? bp : 0];        // offset inside the block-plane
         if (isval && cur != 0) {
-          if (off < 64 && bp < nbp) qs[bp * DQ_PITCH + off] = cur;
+          if (off < 64 && bpok && cur == (int)(int16_t)cur) qs[bp * SYM_QP + off] = (int16_t)cur;
           else bad = true;
         }
-        if (eobf && (off > 64 || bp >= nbp)) bad = true;
+        if (eobf && (off > 64 || !bpok)) bad = true;
         const int tot = __builtin_amdgcn_readlane(incl, 63);
         pcarry += tot & 0xfffff;
         bpcarry += tot >> 20;
-        basecarry = max(basecarry, __builtin_amdgcn_readlane(mx, 63));
-        prevc = __builtin_amdgcn_readlane(cur, 63);
-        cur = nxtv;
       }
-      if (bpcarry != nbp) bad = true;
-      __builtin_amdgcn_wave_barrier();
-      dec_group_math<C, DEC_IMAGE, RGB>(a, G, qs, xs, tq, pos, b, r, lane);
+      prevc = st[SYM_SEG - 1];
     }
+    if (bpcarry != nbp) bad = true;
+    __builtin_amdgcn_wave_barrier();
+    dec_group_math<C, DEC_IMAGE, RGB, int16_t, SYM_QP>(a, G, qs, xs, tq, pos, b, r, lane);
   }
   if (__ballot(bad) && lane == 0) atomicOr(z.fail, 1);
 }

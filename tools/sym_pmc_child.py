@@ -1,6 +1,7 @@
 """Profiling child: the cfg3 entropy stages alone — ZeroRunCoder.encode of the zig-zag
 coefficients (zw_count / scan / zw_emit) and the fused pixels -> symbols path (fused encoder
-OUT_COUNT / scan / OUT_SYMBOLS, then OUT_SYMH with the histogram), once each on 256 (SYM_FRAMES) 4K frames.  Run under
+OUT_COUNT / scan / OUT_SYMBOLS, then OUT_SYMH with the histogram), then
+the decode leg (intra_decode_image of the coefficients, symbols2image of the stream), once each on 256 (SYM_FRAMES) 4K frames.  Run under
 `rocprofv3 --pmc ...`."""
 import os
 import sys
@@ -37,6 +38,14 @@ def main():
     hist = torch.zeros(bench.HIST_BINS + 2, dtype=torch.int64, device=dev)
     D.intra_symbols(frames, table, sym, nsd, hist=hist, hist_lo=bench.HIST_LO - 1)
     torch.cuda.synchronize()
+    if os.environ.get("SYM_DECODE", "1") == "1":
+        # the decode leg: coefficients -> RGB image, and the fused symbols -> RGB image
+        del frames
+        img = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
+        D.intra_decode_image(out, table, img, unzigzag=True, to_rgb=True)
+        err = torch.zeros(3, dtype=torch.int64, device=dev)
+        D.symbols2image(sym, 3, table, img, err, to_rgb=True)
+        torch.cuda.synchronize()
     print("sym_pmc_child done", nsym)
 
 
