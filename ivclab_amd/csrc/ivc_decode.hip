@@ -383,8 +383,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
 
 // group starts from the EOB bit mask of zf_count (bit i of tile t: symbol t * 4096 + i is an
 // EOB slot) and tile_first (EOBs before each tile): the symbol after EOB number C * blk0(g) - 1
-// starts group g; one wave per 4096-symbol tile (lane = 64 symbols), the stream start is group
-// 0's, and the position after the last expected EOB is gstart[ngroups]
+// starts group g; one wave per 4096-symbol tile, lane = 64 symbols.  A lane holds EOBs
+// [e, e + cnt) of the stream; the group starts among their successors are found by arithmetic
+// (one division per lane: the first block-plane >= e + 1 that starts a group, then steps of
+// 8 C block-planes, or to the next block row) and each one's EOB located in the lane's mask.
+// The stream start is group 0's, the position after the last expected EOB is gstart[ngroups].
 __global__ __launch_bounds__(256) void sym_locate_kernel(const uint32_t* __restrict__ mask,
                                                          const int64_t* __restrict__ tile_first,
                                                          int64_t ntiles, int C, int w, int gpr,
@@ -393,20 +396,35 @@ __global__ __launch_bounds__(256) void sym_locate_kernel(const uint32_t* __restr
   const int64_t nwv = (int64_t)gridDim.x * 4;
   if (blockIdx.x == 0 && threadIdx.x == 0) gstart[0] = 0;
   const int64_t D = (int64_t)C * w;                    // block-planes per block row
+  const int64_t GS = 8 * (int64_t)C;                   // block-planes per full group
   for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntiles; t += nwv) {
     const uint64_t mk = (uint64_t)mask[t * 128 + 2 * lane] | ((uint64_t)mask[t * 128 + 2 * lane + 1] << 32);
     const int cnt = __builtin_popcountll(mk);
     const int incl = dec_wave_incl_sum(cnt);
-    int64_t e = tile_first[t] + (incl - cnt);           // EOB index of this lane's first EOB
-    uint64_t m = mk;
-    while (m) {
+    if (cnt == 0) continue;
+    const int64_t e = tile_first[t] + (incl - cnt);   // EOB index of this lane's first EOB
+    // block-plane numbers after this lane's EOBs: (e, e + cnt]
+    const int64_t lo = e + 1, hi = e + cnt < nbp_total ? e + cnt : nbp_total;
+    int64_t row = lo / D;
+    int64_t rem = lo - row * D;
+    rem = (rem + GS - 1) / GS * GS;                    // the first group start at or after lo
+    if (rem >= D) {
+      ++row;
+      rem = 0;
+    }
+    for (int64_t bpn = row * D + rem; bpn <= hi;) {
+      // EOB number bpn - 1 is the lane's (bpn - 1 - e)-th: position of that set bit
+      int k = (int)(bpn - 1 - e);
+      uint64_t m = mk;
+      for (; k > 0; --k) m &= m - 1;
       const int bit = __builtin_ctzll(m);
-      m &= m - 1;
-      const int64_t bpn = e + 1;                          // the block-plane after this EOB
-      ++e;
-      if (bpn > nbp_total) break;
-      const int64_t row = bpn / D, rem = bpn - row * D;
-      if (rem % (8 * C) == 0) gstart[row * gpr + rem / (8 * C)] = t * 4096 + lane * 64 + bit + 1;
+      gstart[row * gpr + rem / GS] = t * 4096 + lane * 64 + bit + 1;
+      rem += GS;
+      if (rem >= D) {
+        ++row;
+        rem = 0;
+      }
+      bpn = row * D + rem;
     }
   }
 }

@@ -722,8 +722,7 @@ constexpr int ZF_TILE = 4096, ZF_HALO = 128;
 __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict__ s, int64_t n,
                                                        int32_t eob, int32_t* __restrict__ tile_eobs,
                                                        int* fail, uint32_t* __restrict__ eobmask) {
-  __shared__ int red[4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
   const int64_t ntiles = (n + ZF_TILE - 1) / ZF_TILE;
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     int cnt = 0;
@@ -740,6 +739,8 @@ __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = i + e < n ? s[i + e] : 1;
       }
+      // (loading the symbol before in every lane, in flight with the quad, measured faster than
+      // taking it from the previous lane by DPP with only lane 0 loading: 3.46 vs 3.79 ms)
       int pv = i > 0 && i < n ? s[i - 1] : 1;       // the stream's first slot is a value slot
       uint32_t bits = 0;
 #pragma unroll
@@ -764,10 +765,7 @@ __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
     if (__ballot(bad) && lane == 0) atomicOr(fail, 1);
-    if (lane == 0) red[wave] = cnt;
-    __syncthreads();
-    if (tid == 0) tile_eobs[t] = red[0] + red[1] + red[2] + red[3];
-    __syncthreads();
+    if (lane == 0 && cnt) atomicAdd(tile_eobs + t, cnt);    // tile_eobs zeroed by the caller
   }
 }
 
@@ -978,6 +976,7 @@ hipError_t launch_zerorun_decode(const int32_t* sym, int64_t n, int64_t expected
     const int64_t ntf = (n + ZF_TILE - 1) / ZF_TILE;
     const unsigned grid = (unsigned)(ntf < 256 * 8 ? ntf : 256 * 8);
     if ((e = hipMemsetAsync(z.flags, 0, 16, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(z.tile_eobs, 0, (size_t)ntf * 4, s)) != hipSuccess) return e;
     zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags, nullptr);
     e = device_scan<int64_t>(ntf, CountGen{z.tile_eobs}, SumI64{}, OffsetSink{z.tile_first, ntf},
                              z.fagg, s);
@@ -1038,6 +1037,7 @@ hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, 
     const int64_t ntf = (n + ZF_TILE - 1) / ZF_TILE;
     const unsigned grid = (unsigned)(ntf < 256 * 8 ? ntf : 256 * 8);
     if ((e = hipMemsetAsync(z.flags, 0, 16, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(z.tile_eobs, 0, (size_t)ntf * 4, s)) != hipSuccess) return e;
     zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags, z.eobmask);
     e = device_scan<int64_t>(ntf, CountGen{z.tile_eobs}, SumI64{}, OffsetSink{z.tile_first, ntf},
                              z.fagg, s);
