@@ -881,10 +881,11 @@ def leg_class_api(args, dev, result, verify):
 
 def make_sharded_step(D, N, seq, pairs, sr, table, mv, q, hist, chunk, hist_wg, zigzag, side):
     """The cfg5 step: ME + MC + residual DCT + quantise of this rank's pairs, then the symbol
-    histograms (coefficients | MV indices).  The pairs go in chunks of `chunk`: ME is
-    VALU-bound and the histogram HBM-bound, so chunk k's histograms run on a side stream
-    (at `hist_wg` workgroups per CU) while chunk k+1 is encoded (same work, same counts:
-    integer adds).  Returns the local histogram (the caller all-gathers it)."""
+    histograms (coefficients | MV indices).  The residual encoder accumulates the
+    coefficients' histogram itself (inter_encode(hist=...): no pass over the 3.2 GB of output
+    per 8-pair chunk); the pairs go in chunks of `chunk` and chunk k's MV-index histogram runs
+    on a side stream (at `hist_wg` workgroups per CU) while chunk k+1 is encoded (same
+    counts: integer adds).  Returns the local histogram (the caller all-gathers it)."""
     def step():
         main = torch.cuda.current_stream()
         L = N.lib()
@@ -895,9 +896,8 @@ def make_sharded_step(D, N, seq, pairs, sr, table, mv, q, hist, chunk, hist_wg, 
             for p0 in range(0, pairs, chunk):
                 p1 = min(p0 + chunk, pairs)
                 D.inter_encode(seq[p0:p1 + 1], sr, table, mv[p0:p1], q[p0:p1], zigzag=zigzag,
-                               stream=main)
+                               stream=main, hist=hist[:HIST_BINS], hist_lo=HIST_LO)
                 side.wait_stream(main)
-                D.histogram(q[p0:p1].view(-1), HIST_LO, hist[:HIST_BINS], stream=side)
                 D.histogram(mv[p0:p1].view(-1), 0, hist[HIST_BINS:], stream=side)
             main.wait_stream(side)
         finally:

@@ -227,6 +227,15 @@ int ivc_motion_compensate_dev(const void* ref, int elem_size, int64_t nframes, i
 int ivc_inter_encode_dev(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W, int sr,
                          const double* table, int calc_dtype, int zigzag, int64_t* mv,
                          int32_t* out, void* stream);
+/* ivc_inter_encode_dev that also accumulates the clamped histogram of the quantised output
+ * (all 3 planes, as written) onto hist[clamp(v - hist_lo, 0, hist_n - 1)] (device int64) in
+ * the encoder itself: the coefficient half of the global Huffman table's input
+ * (ivclab/entropy/entropy.py:6-29 stats_marg over VideoCodec's residual symbols,
+ * ivclab/video/videocodec.py:33,62) without a pass over the output.                   */
+int ivc_inter_encode_hist_dev(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W,
+                              int sr, const double* table, int calc_dtype, int zigzag,
+                              int64_t* mv, int32_t* out, int64_t* hist, int32_t hist_lo,
+                              int32_t hist_n, void* stream);
 
 /* ---------------------------------------------------------------- histogram -------- */
 /* hist[v - lo] += 1 for each symbol (values clamped into [lo, lo+nbins-1]); accumulates.

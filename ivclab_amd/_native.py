@@ -76,6 +76,7 @@ _SIGS = {
     "ivc_motion_compensate": ([_P, _I, _L, _L, _L, _L, _P, _I, _P], _I),
     "ivc_motion_compensate_dev": ([_P, _I, _L, _L, _L, _L, _P, _I, _P, _P], _I),
     "ivc_inter_encode_dev": ([_P, _L, _L, _L, _I, _P, _I, _I, _P, _P, _P], _I),
+    "ivc_inter_encode_hist_dev": ([_P, _L, _L, _L, _I, _P, _I, _I, _P, _P, _P, _I, _I, _P], _I),
     "ivc_histogram_i32": ([_P, _L, _ct.c_int32, _ct.c_int32, _P], _I),
     "ivc_histogram_i32_dev": ([_P, _L, _ct.c_int32, _ct.c_int32, _P, _P], _I),
     "ivc_histogram_i64": ([_P, _L, _L, _ct.c_int32, _P], _I),

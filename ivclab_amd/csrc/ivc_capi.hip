@@ -820,6 +820,27 @@ int ivc_inter_encode_dev(const uint8_t* frames, int64_t nframes, int64_t H, int6
                     "inter_residual");
 }
 
+int ivc_inter_encode_hist_dev(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W, int sr,
+                              const double* table, int calc_dtype, int zigzag, int64_t* mv,
+                              int32_t* out, int64_t* hist, int32_t hist_lo, int32_t hist_n,
+                              void* stream) {
+  TRY(check_frames(nframes, H, W, "inter_encode"));
+  TRY(check_sr(sr));
+  CHECK(calc_dtype == IVC_F64, IVC_E_DTYPE, "inter_encode: float64 residual DCT needs float64 quantisation");
+  CHECK(aligned16(out), IVC_E_ARG, "inter_encode_dev: output must be 16-byte aligned");
+  CHECK(((uintptr_t)frames & 7u) == 0, IVC_E_ARG, "inter_encode_dev: frames must be 8-byte aligned");
+  CHECK(hist && hist_n > 0, IVC_E_ARG, "inter_encode_hist: need a histogram of hist_n > 0 bins");
+  if (nframes < 2) return IVC_OK;
+  QTab t;
+  TRY(load_table(table, &t));
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t HW = H * W;
+  TRY(dev_launch(launch_motion_estimate(frames, frames + HW, IVC_U8, nframes - 1, H, W, sr,
+                                        IVC_ME_EXACT_U8, mv, s), "motion_estimate"));
+  return dev_launch(launch_inter_residual(frames, nframes - 1, H, W, sr, mv, t, zigzag, out, s,
+                                          hist, hist_lo, hist_n), "inter_residual");
+}
+
 // ---------------------------------------------------------------- histogram -----------
 int ivc_histogram_i32_dev(const int32_t* sym, int64_t n, int32_t lo, int32_t nbins, int64_t* hist,
                           void* stream) {

@@ -117,7 +117,8 @@ hipError_t launch_motion_compensate(const void* ref, int esize, int64_t nframes,
                                     hipStream_t s);
 hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W,
                                  int sr, const int64_t* mv, const QTab& t, int zigzag,
-                                 int32_t* out, hipStream_t s);
+                                 int32_t* out, hipStream_t s, int64_t* hist = nullptr,
+                                 int32_t hist_lo = 0, int32_t hist_n = 0);
 
 
 }  // namespace ivc

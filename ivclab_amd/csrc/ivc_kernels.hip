@@ -608,7 +608,10 @@ __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* o
 // OUT_LUMA: the luma-table plane only ([F][h][w][64], 4 B/px out instead of the reference's
 // 12 B/px 3-plane broadcast) — a reported variant, not the reference's output.
 // OUT_SYMH: OUT_SYMBOLS plus the stream's histogram (FusedArgs::zr_hist).
-enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2, OUT_LUMA = 3, OUT_SYMH = 4 };
+// OUT_COEFH: OUT_COEFS plus the coefficients' histogram (FusedArgs::zr_hist), for the
+// residual encoder of the sharded sequence step (the histogram pass over the output it
+// replaces re-read 3.2 GB per 8-pair 8K chunk).
+enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2, OUT_LUMA = 3, OUT_SYMH = 4, OUT_COEFH = 5 };
 
 // Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging.
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
@@ -797,6 +800,36 @@ __device__ __forceinline__ void zr_hist_global(const FusedArgs& a, int64_t v, ui
   __hip_atomic_fetch_add(a.zr_hist + k, (unsigned long long)w, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
 }
+// one symbol (or coefficient) v of weight w into the LDS bins (see above); lanes whose value
+// is out of range add it to the global histogram behind one wave-uniform test
+__device__ __forceinline__ void zh_add(const FusedArgs& a, uint32_t* bins, int32_t v, uint32_t w,
+                                       int lane) {
+  const uint32_t h0 = (uint32_t)(v - ZH_HOT_LO);             // -8..7 -> 0..15
+  const uint32_t hv = v == a.zr_eob ? 16u : (h0 < 16u ? h0 : (uint32_t)ZH_HOT_N);
+  const uint32_t k = (uint32_t)(v + ZH_HALF);
+  const uint32_t kb = hv < (uint32_t)ZH_HOT_N ? ZH_HOT + 32 * hv + (lane & 31)
+                                              : (k < (uint32_t)ZH_BINS ? k : (uint32_t)ZH_TRASH);
+  atomicAdd(bins + kb, w);
+  if (__builtin_expect(__ballot(kb == (uint32_t)ZH_TRASH) != 0, 0)) {
+    if (kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v, w);
+  }
+}
+// the workgroup's bins into the global histogram (after a barrier)
+__device__ __forceinline__ void zh_flush(const FusedArgs& a, const uint32_t* zh, int tid) {
+  for (int i = tid; i < ZH_BINS; i += 256)
+    if (zh[i]) zr_hist_global(a, i - ZH_HALF, zh[i]);
+  for (int i0 = 0; i0 < ZH_HOT_N * 32; i0 += 256) {
+    // the 32 copies of a hot value are 32 consecutive lanes of one wave
+    const int i = i0 + tid;
+    uint32_t c = i < ZH_HOT_N * 32 ? zh[ZH_HOT + i] : 0u;
+#pragma unroll
+    for (int d = 16; d >= 1; d >>= 1) c += __shfl_xor(c, d);
+    if ((i & 31) == 0 && i < ZH_HOT_N * 32 && c) {
+      const int hv = i >> 5;
+      zr_hist_global(a, hv == 16 ? (int64_t)a.zr_eob : (int64_t)(hv + ZH_HOT_LO), c);
+    }
+  }
+}
 
 template <int C, bool DUP, bool HIST>
 __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, int nb,
@@ -822,17 +855,7 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
     for (int j = lane; j < fill; j += 64) {
       const int32_t v = zs[j];
       if (j < lim) a.zr_out[base + j] = v;
-      if constexpr (HIST) {
-        const uint32_t h0 = (uint32_t)(v - ZH_HOT_LO);             // -8..7 -> 0..15
-        const uint32_t hv = v == a.zr_eob ? 16u : (h0 < 16u ? h0 : (uint32_t)ZH_HOT_N);
-        const uint32_t k = (uint32_t)(v + ZH_HALF);
-        const uint32_t kb = hv < (uint32_t)ZH_HOT_N ? ZH_HOT + 32 * hv + (lane & 31)
-                                                    : (k < (uint32_t)ZH_BINS ? k : (uint32_t)ZH_TRASH);
-        atomicAdd(H.bins + kb, 1u);
-        if (__builtin_expect(__ballot(kb == (uint32_t)ZH_TRASH) != 0, 0)) {
-          if (kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v, 1u);
-        }
-      }
+      if constexpr (HIST) zh_add(a, H.bins, v, 1u, lane);
     }
     __builtin_amdgcn_wave_barrier();
     base += fill;
@@ -944,19 +967,36 @@ __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b,
   if (lane == 0) a.zr_counts[gid] = v;
 }
 
+// OUT_COEFH: the staged group's coefficients into the histogram bins (plane 1 twice when it
+// is also stored as plane 2); blocks past the frame's edge are not counted
+template <int C, bool DUP>
+__device__ __forceinline__ void coef_hist(const FusedArgs& a, const int32_t* os, int nb,
+                                          uint32_t* bins) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;
+  constexpr int PITCH = os_pitch<C, DUP>();
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    if (b >= nb) break;                         // wave-uniform
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+      zh_add(a, bins, os[b * PITCH + p * 64 + lane], (C == 1 && DUP && p == 1) ? 2u : 1u, lane);
+  }
+}
+
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
           int NG, bool DUP, int OUTM = OUT_COEFS>
 __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) {
-  static_assert(OUTM == OUT_COEFS || OUTM == OUT_LUMA || (ZZ && SRC == SRC_IMAGE),
+  static_assert(OUTM == OUT_COEFS || OUTM == OUT_LUMA || OUTM == OUT_COEFH || (ZZ && SRC == SRC_IMAGE),
                 "symbols need zig-zag order");
   static_assert(OUTM != OUT_LUMA || C == 1, "the luma-only output is for C = 1 images");
-  constexpr bool COEF = OUTM == OUT_COEFS || OUTM == OUT_LUMA;
+  constexpr bool COEF = OUTM == OUT_COEFS || OUTM == OUT_LUMA || OUTM == OUT_COEFH;
   constexpr bool SYM = OUTM == OUT_SYMBOLS || OUTM == OUT_SYMH;   // emission pass
   typedef WaveLds<T, C, DUP> L;
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
   __shared__ double srq[FAST ? 192 : 1];
   __shared__ D sq[192];
-  __shared__ uint32_t zh[OUTM == OUT_SYMH ? ZH_LDS : 1];
+  __shared__ uint32_t zh[OUTM == OUT_SYMH || OUTM == OUT_COEFH ? ZH_LDS : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   const int b = lane >> 3, r = lane & 7;
@@ -980,7 +1020,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
     }
   }
   ZrHistAcc hacc{nullptr};
-  if constexpr (OUTM == OUT_SYMH) {
+  if constexpr (OUTM == OUT_SYMH || OUTM == OUT_COEFH) {
     for (int i = tid; i < ZH_LDS; i += 256) zh[i] = 0;
     hacc.bins = zh;
   }
@@ -1059,6 +1099,9 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
           RowReg<TI, C, SRC> v;
           group_row<TI, C, NG>(ring[p], g, lane, v);
           encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+          if constexpr (OUTM == OUT_COEFH) {
+            if (ex) coef_hist<C, DUP>(a, os, group_loc<NG>(a, tp, g).nb, hacc.bins);
+          }
           if constexpr (!COEF) {
             if (ex) zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, tp, g).nb, (int64_t)tp * NG + g, hacc);
           }
@@ -1100,6 +1143,7 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
           gather_inter(a, lt, b, r, v);
         }
         encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+        if constexpr (OUTM == OUT_COEFH) coef_hist<C, DUP>(a, os, group_loc<NG>(a, lt, g).nb, hacc.bins);
         if constexpr (!COEF)
           zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, lt, g).nb, (int64_t)lt * NG + g, hacc);
         plt = lt;
@@ -1130,21 +1174,9 @@ __global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) 
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
-  if constexpr (OUTM == OUT_SYMH) {
+  if constexpr (OUTM == OUT_SYMH || OUTM == OUT_COEFH) {
     __syncthreads();
-    for (int i = tid; i < ZH_BINS; i += 256)
-      if (zh[i]) zr_hist_global(a, i - ZH_HALF, zh[i]);
-    for (int i0 = 0; i0 < ZH_HOT_N * 32; i0 += 256) {
-      // the 32 copies of a hot value are 32 consecutive lanes of one wave
-      const int i = i0 + tid;
-      uint32_t c = i < ZH_HOT_N * 32 ? zh[ZH_HOT + i] : 0u;
-#pragma unroll
-      for (int d = 16; d >= 1; d >>= 1) c += __shfl_xor(c, d);
-      if ((i & 31) == 0 && i < ZH_HOT_N * 32 && c) {
-        const int hv = i >> 5;
-        zr_hist_global(a, hv == 16 ? (int64_t)a.zr_eob : (int64_t)(hv + ZH_HOT_LO), c);
-      }
-    }
+    zh_flush(a, zh, tid);
   }
 }
 
@@ -1751,12 +1783,26 @@ hipError_t launch_intra_symbols(const void* img, int dtype, int64_t nframes, int
 
 hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W,
                                  int sr, const int64_t* mv, const QTab& t_in, int zigzag,
-                                 int32_t* out, hipStream_t s) {
+                                 int32_t* out, hipStream_t s, int64_t* hist, int32_t hist_lo,
+                                 int32_t hist_n) {
   if (nframes <= 0) return hipSuccess;
   const QTab& t = t_in;
   FusedArgs a = make_fused_args(frames, mv, out, nframes, H, W, sr, t);
   const int64_t ntiles = nframes * (int64_t)a.h * a.tpr;
   if (ntiles >= (1LL << 31)) return hipErrorInvalidValue;  // 32-bit tile indices
+  if (hist && hist_n > 0) {
+    // the coefficients' histogram accumulated by the encoder itself (OUT_COEFH)
+    a.zr_hist = reinterpret_cast<unsigned long long*>(hist);
+    a.zr_hist_lo = hist_lo;
+    a.zr_hist_n = hist_n;
+    const bool cm = needs_magnitude_check(t);
+#define RES_H(ZZV, CMV) \
+  launch_fused_one<int16_t, double, double, 1, true, ZZV, SRC_INTER, CMV, IVC_WIDE_NG, OUT_COEFH>(a, t, s)
+    if (zigzag) { if (cm) RES_H(true, true); else RES_H(true, false); }
+    else { if (cm) RES_H(false, true); else RES_H(false, false); }
+#undef RES_H
+    return hipGetLastError();
+  }
   launch_fused_zz<int16_t, double, double, 1, true, SRC_INTER>(a, t, zigzag, ntiles, s);
   return hipGetLastError();
 }

@@ -58,13 +58,25 @@ def intra_encode(img, table, out, zigzag=False, hist=None, hist_lo=0, stream=Non
                                          hist_lo, nb, _stream(stream)), "intra_encode")
 
 
-def inter_encode(frames, sr, table, mv, out, zigzag=False, stream=None):
+def inter_encode(frames, sr, table, mv, out, zigzag=False, stream=None, hist=None, hist_lo=0):
     """frames [F, H, W] uint8 -> mv [F-1, H/8, W/8] int64 and out [F-1, H/8, W/8, 3, 64]:
-    ME(frames[f-1], frames[f]) (exact SSD) -> MC -> residual -> DCT -> quantize."""
+    ME(frames[f-1], frames[f]) (exact SSD) -> MC -> residual -> DCT -> quantize.  hist
+    (optional, int64 [n]): the output's histogram is accumulated onto hist[clamp(v - hist_lo,
+    0, n - 1)] by the encoder itself (no pass over out)."""
     for t_, n in ((frames, "frames"), (mv, "mv"), (out, "out")):
         _contig(t_, n)
     F, H, W = frames.shape
     t = N.table_arg(table)
+    if hist is not None:
+        import torch
+        _contig(hist, "hist")
+        if hist.dtype != torch.int64 or hist.numel() < 1:
+            raise ValueError("inter_encode: hist must be a non-empty int64 tensor")
+        N.check(N.lib().ivc_inter_encode_hist_dev(frames.data_ptr(), F, H, W, int(sr), N.ptr(t),
+                                                  N.F64, int(bool(zigzag)), mv.data_ptr(),
+                                                  out.data_ptr(), hist.data_ptr(), int(hist_lo),
+                                                  hist.numel(), _stream(stream)), "inter_encode")
+        return
     N.check(N.lib().ivc_inter_encode_dev(frames.data_ptr(), F, H, W, int(sr), N.ptr(t), N.F64,
                                          int(bool(zigzag)), mv.data_ptr(), out.data_ptr(),
                                          _stream(stream)), "inter_encode")

@@ -1399,3 +1399,41 @@ def test_me_float_search_device_frames_and_1080p():
         for rows in ((0, 3), (67, 70), (132, 135)):
             want = c_motion_vectors(fr[p], fr[p + 1], 16, rows=rows)[..., 0]
             assert_bits(got[p, rows[0]:rows[1]], want, f"pair {p} rows {rows}")
+
+
+@pytest.mark.parametrize("zz", [0, 1])
+@pytest.mark.parametrize("case", ["jpeg", "fine", "custom"])
+def test_inter_encode_encoder_histogram(zz, case):
+    """ivc_inter_encode_hist_dev (the residual encoder accumulating its output's histogram,
+    OUT_COEFH; ivclab/entropy/entropy.py:6-29 over VideoCodec's residual coefficients): the
+    output equals ivc_inter_encode_dev's and the histogram equals the oracle's histogram of it,
+    clamped into [lo, lo + n) for a wide and a narrow range; a ragged block row (19 blocks),
+    values far outside the LDS bins (scale 0.013: the global-atomic path) and a table whose
+    planes 1 and 2 differ (3 staged planes instead of plane 1 counted twice)."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    rng = np.random.default_rng(31 + 7 * zz + len(case))
+    F, H, W, sr = 3, 48, 152, 4
+    base = rng.integers(0, 256, (H + 16, W + 16)).astype(np.int16)
+    frames = np.stack([np.clip(base[4 + f:4 + f + H, 2 * f:2 * f + W] + rng.integers(-9, 10, (H, W)),
+                               0, 255) for f in range(F)]).astype(np.uint8)
+    scale = {"jpeg": 1.0, "fine": 0.013, "custom": 0.5}[case]
+    table = PatchQuant(scale).get_quantization_table().astype(np.float64)
+    if case == "custom":
+        table[2] *= 1.37
+    fr = torch.from_numpy(frames).cuda()
+    mv0 = torch.empty((F - 1, H // 8, W // 8), dtype=torch.int64, device="cuda")
+    q0 = torch.empty((F - 1, H // 8, W // 8, 3, 64), dtype=torch.int32, device="cuda")
+    D.inter_encode(fr, sr, table, mv0, q0, zigzag=bool(zz))
+    for lo, n in [(-4097, 8194), (-3, 9)]:
+        mv = torch.empty_like(mv0)
+        q = torch.empty_like(q0)
+        hist = torch.zeros(n, dtype=torch.int64, device="cuda")
+        D.inter_encode(fr, sr, table, mv, q, zigzag=bool(zz), hist=hist, hist_lo=lo)
+        torch.cuda.synchronize()
+        assert_bits(q.cpu().numpy(), q0.cpu().numpy(), f"q {case} zz={zz}")
+        assert_bits(mv.cpu().numpy(), mv0.cpu().numpy(), f"mv {case} zz={zz}")
+        want = O.histogram(q0.cpu().numpy().reshape(-1), lo, n)
+        assert np.array_equal(hist.cpu().numpy(), want), (case, zz, lo, n)
+    if case == "fine":
+        assert np.abs(q0.cpu().numpy()).max() > 600          # the out-of-range path ran

@@ -185,7 +185,8 @@ def test_chunked_inter_encode_with_side_stream_histograms():
     """The cfg5 step shape: inter_encode in chunks of 2 pairs with each chunk's coefficient
     and motion-vector histograms on a side stream while the next chunk is encoded, at reduced
     histogram occupancy, gives the same mv, q and histograms as one call followed by the
-    histograms on the main stream."""
+    histograms on the main stream; and with the coefficients' histogram accumulated by the
+    encoder itself (inter_encode(hist=...), the bench's form) the histogram is the same."""
     import ivclab_amd._native as N
     dev = torch.device("cuda:0")
     F, H, W, sr = 7, 1080, 1920, 16
@@ -193,7 +194,7 @@ def test_chunked_inter_encode_with_side_stream_histograms():
     P = F - 1
     nmv = (2 * sr + 1) ** 2
 
-    def run(chunk, wg):
+    def run(chunk, wg, enc_hist=False):
         mv = torch.empty((P, H // 8, W // 8), dtype=torch.int64, device=dev)
         q = torch.empty((P, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
         hist = torch.zeros(bench.HIST_BINS + nmv, dtype=torch.int64, device=dev)
@@ -204,9 +205,14 @@ def test_chunked_inter_encode_with_side_stream_histograms():
         try:
             for p0 in range(0, P, chunk):
                 p1 = min(p0 + chunk, P)
-                D.inter_encode(seq[p0:p1 + 1], sr, TABLE, mv[p0:p1], q[p0:p1], stream=main)
+                if enc_hist:
+                    D.inter_encode(seq[p0:p1 + 1], sr, TABLE, mv[p0:p1], q[p0:p1], stream=main,
+                                   hist=hist[:bench.HIST_BINS], hist_lo=bench.HIST_LO)
+                else:
+                    D.inter_encode(seq[p0:p1 + 1], sr, TABLE, mv[p0:p1], q[p0:p1], stream=main)
                 side.wait_stream(main)
-                D.histogram(q[p0:p1].view(-1), bench.HIST_LO, hist[:bench.HIST_BINS], stream=side)
+                if not enc_hist:
+                    D.histogram(q[p0:p1].view(-1), bench.HIST_LO, hist[:bench.HIST_BINS], stream=side)
                 D.histogram(mv[p0:p1].view(-1), 0, hist[bench.HIST_BINS:], stream=side)
             main.wait_stream(side)
             torch.cuda.synchronize()
@@ -216,9 +222,12 @@ def test_chunked_inter_encode_with_side_stream_histograms():
 
     mv1, q1, h1 = run(P, 0)
     mv2, q2, h2 = run(2, 2)
+    mv3, q3, h3 = run(2, 2, enc_hist=True)
     assert_bits(mv2, mv1, "mv chunked")
     assert_bits(q2, q1, "q chunked")
     assert_bits(h2, h1, "hist chunked")
+    assert_bits(q3, q1, "q chunked, encoder histogram")
+    assert_bits(h3, h1, "hist chunked, encoder histogram")
     assert h1[:bench.HIST_BINS].sum() == q1.size and h1[bench.HIST_BINS:].sum() == mv1.size
     assert np.array_equal(h1[bench.HIST_BINS:], O.histogram(mv1, 0, nmv))
     assert np.array_equal(h1[:bench.HIST_BINS], O.histogram(q1, bench.HIST_LO, bench.HIST_BINS))
