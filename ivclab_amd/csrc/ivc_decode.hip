@@ -272,7 +272,6 @@ struct SymImageArgs {
 // in the region the IDCT's transpose uses afterwards — and parsed from there (a first version
 // loaded 64 symbols per iteration, one HBM latency per chunk: 25 ms for the cfg3 stream).
 constexpr int SYM_SEG = 1280;                          // symbols staged per round (5 KB)
-static_assert(SYM_SEG % 256 == 0, "the parse takes 256 symbols per wave-iteration");
 // coefficients staged as int16 (a value outside int16 sends the stream to the general path):
 // half the LDS of int32 rows, 4 workgroups per CU instead of 3
 constexpr int SYM_QP = 72;                             // int16 per staged block-plane (144 B)
@@ -344,53 +343,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
       }
       __builtin_amdgcn_wave_barrier();
       const int rlen = len - s0 < SYM_SEG ? len - s0 : SYM_SEG;
-      // 4 symbols per lane, 256 per wave-iteration: the per-symbol typing is lane-local, one
-      // DPP scan covers the lane totals (a first form with one symbol per lane issued ~45 VALU
-      // per 64 symbols)
-      for (int c0 = 0; c0 < rlen; c0 += 256) {
-        const int i0 = c0 + 4 * lane;
-        const int4 q4 = *reinterpret_cast<const int4*>(st + i0);
-        const int sv[4] = {q4.x, q4.y, q4.z, q4.w};
-        const int prv0 = st[i0 - 1], nx3 = st[i0 + 4];
-        bool eo[4], nzv[4];
-        int lp[4];
-        int ptot = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int pv = k == 0 ? prv0 : sv[k - 1];
-          const int nv = k == 3 ? nx3 : sv[k + 1];
-          const bool valid = i0 + k < rlen;
-          const bool rl = pv == 0;                     // a run-length slot
-          eo[k] = valid && !rl && sv[k] == z.eob;
-          const bool isval = valid && !rl && !eo[k];
-          nzv[k] = isval && sv[k] != 0;
-          const int run = nv < 1 ? 1 : (nv > 4095 ? 4095 : nv);
-          const int cc = isval ? (sv[k] == 0 ? run : 1) : 0;
-          lp[k] = ptot;
-          ptot += (eo[k] ? (1 << 20) : 0) | cc;
-        }
-        const int incl = dec_wave_incl_sum(ptot);
-        const int excl = incl - ptot;
-        int pex[4], bp[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int ex = excl + lp[k];
-          pex[k] = pcarry + (ex & 0xfffff);             // the slot's coefficient offset
-          bp[k] = bpcarry + (ex >> 20);                 // its block-plane
-          // block-plane starts through LDS: an EOB records where the next block-plane starts
-          if (eo[k] && bp[k] < nbp) bps[bp[k] + 1] = pex[k];
-        }
+      for (int c0 = 0; c0 < rlen; c0 += 64) {
+        const int i = c0 + lane;
+        const int cur = st[i], prv = st[i - 1], nx = st[i + 1];
+        const bool valid = i < rlen;
+        const bool rl = prv == 0;                      // a run-length slot
+        const bool eobf = valid && !rl && cur == z.eob;
+        const bool isval = valid && !rl && !eobf;
+        const int run = nx < 1 ? 1 : (nx > 4095 ? 4095 : nx);
+        const int cc = isval ? (cur == 0 ? run : 1) : 0;
+        const int packed = (eobf ? (1 << 20) : 0) | cc;
+        const int incl = dec_wave_incl_sum(packed);
+        const int excl = incl - packed;
+        const int pex = pcarry + (excl & 0xfffff);     // this slot's coefficient offset
+        const int bp = bpcarry + (excl >> 20);          // its block-plane
+        // block-plane starts through LDS: an EOB lane records where the next block-plane
+        // starts, then every lane reads its own block-plane's start (in-order LDS per wave)
+        const bool bpok = bp < nbp;
+        if (eobf && bpok) bps[bp + 1] = pex;
         __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const bool bpok = bp[k] < nbp;
-          const int off = pex[k] - bps[bpok ? bp[k] : 0];   // offset inside the block-plane
-          if (nzv[k]) {
-            if (off < 64 && bpok && sv[k] == (int)(int16_t)sv[k]) qs[bp[k] * SYM_QP + off] = (int16_t)sv[k];
-            else bad = true;
-          }
-          if (eo[k] && (off > 64 || !bpok)) bad = true;
+        const int off = pex - bps[bpok ? bp : 0];        // offset inside the block-plane
+        if (isval && cur != 0) {
+          if (off < 64 && bpok && cur == (int)(int16_t)cur) qs[bp * SYM_QP + off] = (int16_t)cur;
+          else bad = true;
         }
+        if (eobf && (off > 64 || !bpok)) bad = true;
         const int tot = __builtin_amdgcn_readlane(incl, 63);
         pcarry += tot & 0xfffff;
         bpcarry += tot >> 20;
