@@ -100,7 +100,10 @@ __device__ __forceinline__ void dec_load(const DecArgs& a, int64_t g, int lane, 
 // qs + (b * C + p) * DQ_PITCH, zig-zag or raster order inside) and its output: DEC_BLOCKS
 // [nblk][3][8][8] or DEC_IMAGE rows.  Shared by intra_decode_kernel (coefficients from HBM) and
 // sym_image_kernel (coefficients expanded from the zero-run stream).
-template <int C, int OUTL, bool RGB, typename Q = int32_t, int QP = DQ_PITCH>
+// FASTDQ: |q * table| < 2^31 is known (int16 coefficients, finite |table| < 2^16, checked on
+// the host), so NumPy's float64 -> int32 cast of the dequantised value is a truncation
+// (v_trunc_f64) with no range handling.
+template <int C, int OUTL, bool RGB, typename Q = int32_t, int QP = DQ_PITCH, bool FASTDQ = false>
 __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup& G,
                                                const Q* qs, double* xs, const double* tq,
                                                const uint32_t* pos, int b, int r, int lane) {
@@ -115,8 +118,12 @@ __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup&
     }
     double x[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k)   // patchquant.py:77-78: int32 * table (float64), truncated
-      x[k] = (double)np_to_i32<double>((double)qv[k] * tq[p * 64 + r * 8 + k]);
+    for (int k = 0; k < 8; ++k) {  // patchquant.py:77-78: int32 * table (float64), truncated
+      if constexpr (FASTDQ)   // + 0.0: a truncated -0.x is -0.0, the int32 round trip gives +0.0
+        x[k] = __builtin_trunc((double)qv[k] * tq[p * 64 + r * 8 + k]) + 0.0;
+      else
+        x[k] = (double)np_to_i32<double>((double)qv[k] * tq[p * 64 + r * 8 + k]);
+    }
     dct3_line<double>(x, 0.25, true);                 // axis -1 (row r)
 #pragma unroll
     for (int k = 0; k < 8; ++k) xs[b * 72 + r * 9 + k] = x[k];
@@ -155,9 +162,13 @@ __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup&
         v[0] = Y + 1.402 * Cr;
         v[1] = (Y - 0.344136 * Cb) - 0.714136 * Cr;
         v[2] = Y + 1.772 * Cb;
+        // np.clip(v, 0, 255): the dequantised values are finite int32s, so v is finite (no
+        // NaN case); min keeps -0.0 (np.clip keeps it too), negatives become +0.0
 #pragma unroll
-        for (int c = 0; c < 3; ++c)
-          o[c][i] = v[c] != v[c] ? v[c] : (v[c] < 0.0 ? 0.0 : (v[c] > 255.0 ? 255.0 : v[c]));
+        for (int c = 0; c < 3; ++c) {
+          const double m = __builtin_fmin(v[c], 255.0);
+          o[c][i] = m < 0.0 ? 0.0 : m;
+        }
       }
     }
     // two image rows at a time: stage [ri][px = 8 b + r][p], then 16-byte stores of the
@@ -278,7 +289,7 @@ constexpr int SYM_QP = 72;                             // int16 per staged block
 constexpr int SYM_XW = SYM_SEG + 8;                    // int32 words: [3] = prev, [4 ..] symbols
 constexpr int SYM_XD = (SYM_XW / 2 > DX_WAVE ? SYM_XW / 2 : DX_WAVE);   // doubles per wave
 
-template <int C, bool RGB>
+template <int C, bool RGB, bool FASTDQ>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t) {
   constexpr int QS = 8 * C * SYM_QP;                   // int16 per wave
   __shared__ __attribute__((aligned(16))) int16_t qs_all[4 * QS];
@@ -376,7 +387,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     }
     if (bpcarry != nbp) bad = true;
     __builtin_amdgcn_wave_barrier();
-    dec_group_math<C, DEC_IMAGE, RGB, int16_t, SYM_QP>(a, G, qs, xs, tq, pos, b, r, lane);
+    dec_group_math<C, DEC_IMAGE, RGB, int16_t, SYM_QP, FASTDQ>(a, G, qs, xs, tq, pos, b, r, lane);
   }
   if (__ballot(bad) && lane == 0) atomicOr(z.fail, 1);
 }
@@ -500,10 +511,16 @@ hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const ui
     const unsigned grid = resident_grid_ptr(reinterpret_cast<const void*>(k), (a.ngroups + 3) / 4);
     k<<<grid, 256, 0, s>>>(a, z, t);
   };
+  // int16 coefficients times a finite table below 2^16 in magnitude stay inside int32
+  bool fast = true;
+  for (int i = 0; i < 192; ++i)
+    if (!(__builtin_fabs(t.q[i]) < 65536.0)) fast = false;
   if (C == 3) {
-    if (to_rgb) go(sym_image_kernel<3, true>); else go(sym_image_kernel<3, false>);
+    if (to_rgb) { if (fast) go(sym_image_kernel<3, true, true>); else go(sym_image_kernel<3, true, false>); }
+    else { if (fast) go(sym_image_kernel<3, false, true>); else go(sym_image_kernel<3, false, false>); }
   } else {
-    if (to_rgb) go(sym_image_kernel<1, true>); else go(sym_image_kernel<1, false>);
+    if (to_rgb) { if (fast) go(sym_image_kernel<1, true, true>); else go(sym_image_kernel<1, true, false>); }
+    else { if (fast) go(sym_image_kernel<1, false, true>); else go(sym_image_kernel<1, false, false>); }
   }
   return hipGetLastError();
 }

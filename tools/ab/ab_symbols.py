@@ -1,6 +1,6 @@
 """Same-process A/B timing of libivc variants (ab/*.so) on the symbol legs of bench.py: the
 zero-run encode of the cfg3 zig-zag coefficients, the fused pixels -> symbols path (without and with the
-emission pass's histogram), the symbol histogram and min/max.  Every variant's outputs are compared with the first one's.
+emission pass's histogram), symbols -> RGB image, the symbol histogram and min/max.  Every variant's outputs are compared with the first one's.
     python tools/ab/ab_symbols.py ab/base.so ab/new.so [--frames 256] [--rounds 5]"""
 import argparse
 import ctypes
@@ -49,6 +49,8 @@ nsd = torch.zeros(1, dtype=torch.int64, device=dev)
 hist = torch.zeros(4200, dtype=torch.int64, device=dev)
 mm = torch.empty(2, dtype=torch.int32, device=dev)
 hist2 = torch.zeros(8194, dtype=torch.int64, device=dev)
+img = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
+err = torch.zeros(3, dtype=torch.int64, device=dev)
 
 
 def timeit(fn, reps=3):
@@ -71,6 +73,9 @@ legs = {
     "symbols_hist": lambda L: (hist2.zero_(), N.check(L.ivc_intra_symbols_hist_dev(
         img.data_ptr(), 1, F, H, W, 1, t.ctypes.data, 4000, sym.data_ptr(), nsym, nsd.data_ptr(),
         hist2.data_ptr(), -4097, 8194, stream))),
+    "symbols2image": lambda L: N.check(L.ivc_symbols2image_dev(
+        sym.data_ptr(), nsym, F, H, W, 3, t.ctypes.data, 4000, 1, img.data_ptr(), err.data_ptr(),
+        stream)),
     "histogram": lambda L: (hist.zero_(), N.check(L.ivc_histogram_i32_dev(
         sym.data_ptr(), nsym, -64, 4200, hist.data_ptr(), stream))),
     "minmax": lambda L: N.check(L.ivc_minmax_i32_dev(sym.data_ptr(), nsym, mm.data_ptr(), stream)),
@@ -84,8 +89,10 @@ for rnd in range(args.rounds):
             if rnd == 0:
                 torch.cuda.synchronize()
                 outs = {"zerorun_encode": sym, "intra_symbols": sym, "symbols_hist": hist2,
-                        "histogram": hist, "minmax": mm}
-                digest = (int(outs[leg].view(-1)[:1 << 24].to(torch.int64).sum().item()),
+                        "symbols2image": img, "histogram": hist, "minmax": mm}
+                o = outs[leg].view(-1)[:1 << 24]
+                o = o.view(torch.int64) if o.dtype == torch.float64 else o.to(torch.int64)
+                digest = (int(o.sum().item()),
                           int(outs[leg].numel()))
                 check.setdefault(leg, digest)
                 if digest != check[leg]:
