@@ -786,7 +786,7 @@ __device__ __forceinline__ int sym_read_addr(int k) {
 // block-plane around the LDS atomic — ~13 scalar instructions each on the co-critical scalar
 // unit, emission 4.9 -> 8.0 ms — and a branch-free per-block-plane add — ~8 VALU per
 // block-plane, 7.66 ms.)
-constexpr int ZH_HALF = 512, ZH_BINS = 2 * ZH_HALF;
+constexpr int ZH_HALF = 128, ZH_BINS = 2 * ZH_HALF;
 constexpr int ZH_HOT_LO = -8, ZH_HOT_N = 17;            // -8..7, and the EOB as hot value 16
 constexpr int ZH_HOT = ZH_BINS;                           // 32 copies per hot value
 constexpr int ZH_TRASH = ZH_HOT + 32 * ZH_HOT_N;          // out-of-range values (uncounted)
@@ -986,7 +986,7 @@ __device__ __forceinline__ void coef_hist(const FusedArgs& a, const int32_t* os,
 
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
           int NG, bool DUP, int OUTM = OUT_COEFS>
-__global__ __launch_bounds__(256) void fused_encode_kernel(FusedArgs a, QTab t) {
+__global__ __launch_bounds__(256, (OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) ? 6 : 1) void fused_encode_kernel(FusedArgs a, QTab t) {
   static_assert(OUTM == OUT_COEFS || OUTM == OUT_LUMA || OUTM == OUT_COEFH || (ZZ && SRC == SRC_IMAGE),
                 "symbols need zig-zag order");
   static_assert(OUTM != OUT_LUMA || C == 1, "the luma-only output is for C = 1 images");
