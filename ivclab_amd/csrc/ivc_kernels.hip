@@ -986,7 +986,7 @@ __device__ __forceinline__ void coef_hist(const FusedArgs& a, const int32_t* os,
 
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
           int NG, bool DUP, int OUTM = OUT_COEFS>
-__global__ __launch_bounds__(256, (OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) ? 6 : 1) void fused_encode_kernel(FusedArgs a, QTab t) {
+__global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && C == 1 && DUP) ? 6 : 1) void fused_encode_kernel(FusedArgs a, QTab t) {
   static_assert(OUTM == OUT_COEFS || OUTM == OUT_LUMA || OUTM == OUT_COEFH || (ZZ && SRC == SRC_IMAGE),
                 "symbols need zig-zag order");
   static_assert(OUTM != OUT_LUMA || C == 1, "the luma-only output is for C = 1 images");
