@@ -739,9 +739,13 @@ __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = i + e < n ? s[i + e] : 1;
       }
-      // (loading the symbol before in every lane, in flight with the quad, measured faster than
-      // taking it from the previous lane by DPP with only lane 0 loading: 3.46 vs 3.79 ms)
-      int pv = i > 0 && i < n ? s[i - 1] : 1;       // the stream's first slot is a value slot
+      // the symbol before: the previous lane's last (DPP); lane 0's comes from one scalar load
+      // per wave (a wave-uniform address), issued with the quads — not a per-lane load (one
+      // dword load per lane doubled the vector memory instructions), nor a lane-0 vector load
+      // after the quad (a second latency: 3.79 vs 3.46 ms)
+      const int64_t iw = (int64_t)__builtin_amdgcn_readfirstlane((int)(i - t * ZF_TILE)) + t * ZF_TILE;
+      const int p0 = iw > 0 && iw <= n ? s[iw - 1] : 1;   // the stream's first slot is a value slot
+      int pv = __builtin_amdgcn_update_dpp(p0, v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
       uint32_t bits = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
