@@ -86,7 +86,13 @@ def launcher_cmd(n, argv, port):
             os.path.abspath(__file__)] + list(argv)
 
 
-def dist_setup(n_gpus):
+# --rccl: at one rank, a one-rank RCCL process group so the exchange's collectives still run
+# through RCCL (dist stays None for the bench's own one-rank logic)
+FORCE_COLL = False
+
+
+def dist_setup(n_gpus, rccl_world1=False):
+    global FORCE_COLL
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -105,10 +111,16 @@ def dist_setup(n_gpus):
             dist.init_process_group(backend)
         return dist, rank, world, dev
     torch.cuda.set_device(0)
+    if rccl_world1:
+        from ivclab_amd.distributed import init_single_rank
+        init_single_rank("cuda:0")
+        FORCE_COLL = True
     return None, 0, 1, 0
 
 
 def coll_name(dist):
+    if dist is None:
+        return "RCCL, 1 rank" if FORCE_COLL else "none (1 rank)"
     b = dist.get_backend()
     return "RCCL" if b == "nccl" else b
 
@@ -602,7 +614,7 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
         # the emission pass's histogram over the fixed range [HIST_LO, HIST_LO + HIST_BINS) with
         # a guard bin at each end, one all-gather; the alphabet bounds (min - 20, max + 21:
         # intracodec.py:161-166) come from its first and last nonzero bins
-        g = global_histogram(hist).cpu().numpy()
+        g = global_histogram(hist, force=FORCE_COLL).cpu().numpy()
         bnd = bounds_from_histogram(g, HIST_LO)
         if bnd is not None:
             b0_, b1_ = huffman_bounds(*bnd)
@@ -611,11 +623,11 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
         # histogram over them (an all-reduce and an all-gather)
         fallback["used"] = True
         D.minmax(sym, mm)
-        lo, hi = global_bounds(mm)
+        lo, hi = global_bounds(mm, force=FORCE_COLL)
         b0_, b1_ = huffman_bounds(lo, hi)
         h2 = torch.zeros(b1_ - b0_ - 1, dtype=torch.int64, device=dev)
         D.histogram(sym, b0_, h2)
-        return b0_, b1_, global_histogram(h2).cpu().numpy()
+        return b0_, b1_, global_histogram(h2, force=FORCE_COLL).cpu().numpy()
 
     exchange()                      # warm-up: first-launch and allocator costs stay untimed
     torch.cuda.synchronize()
@@ -670,7 +682,7 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
         "histogram": "accumulated by the image2symbols emission pass (LDS bins, flushed per workgroup)",
         "collective": (f"all_gather_into_tensor ({coll_name(dist)}), {HIST_BINS + 2} int64 bins"
                        if not fallback["used"] else f"all_reduce + all_gather ({coll_name(dist)})")
-        if dist is not None else "none (1 rank)"}
+        if dist is not None or FORCE_COLL else "none (1 rank)"}
     return sym
 
 
@@ -925,7 +937,7 @@ def leg_sharded(args, dist, rank, world, dev, table, result, verify):
                               args.sharded_hist_wg, args.zigzag, side)
 
     def sstep():
-        return global_histogram(local())
+        return global_histogram(local(), force=FORCE_COLL)
 
     swall, _ = timed(dist, sstep, args.sharded_steps, 1)
     g5 = sstep()
@@ -942,7 +954,7 @@ def leg_sharded(args, dist, rank, world, dev, table, result, verify):
                                f"rank(s) (+1 halo frame each), sr={sr5}",
                    "pairs_per_rank_max": int(max_over_ranks(dist, float(pairs5)))},
         "exchange": {"collective": f"all_gather_into_tensor ({coll_name(dist)})"
-                     if dist is not None else "none (1 rank)",
+                     if dist is not None or FORCE_COLL else "none (1 rank)",
                      "bins": HIST_BINS + nmv,
                      "symbols": int(g5h[:HIST_BINS].sum()),
                      "motion_vectors": int(g5h[HIST_BINS:].sum()),
@@ -1013,6 +1025,8 @@ def parse(argv=None):
     ap.add_argument("--no-luma", action="store_true", help="skip the luma-only (5 B/px) leg")
     ap.add_argument("--no-class-api", action="store_true", help="skip the host-buffer leg")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--rccl", action="store_true",
+                    help="at 1 rank, run the histogram exchange through a one-rank RCCL group")
     ap.add_argument("--no-sharded", action="store_true", help="skip the cfg5 8K leg")
     ap.add_argument("--no-cpu-pool", action="store_true", help="skip the multi-core CPU leg")
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle checks")
@@ -1046,7 +1060,7 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # start the ranks ourselves (nothing has touched the GPU yet) and pass their status on
         sys.exit(subprocess.call(launcher_cmd(args.gpus, sys.argv[1:], free_port())))
-    dist, rank, world, local = dist_setup(args.gpus)
+    dist, rank, world, local = dist_setup(args.gpus, rccl_world1=args.rccl)
     dev = torch.device("cuda", torch.cuda.current_device())
     from ivclab_amd import PatchQuant
     table = PatchQuant(1.0).get_quantization_table()
@@ -1139,8 +1153,9 @@ def main():
     result["bench_wall_s"] = round(time.perf_counter() - t_start, 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if dist is not None or FORCE_COLL:
+        import torch.distributed as tdist
+        tdist.destroy_process_group()
     if verify is not None and result["verify"]["ok"] is False:
         sys.exit(3)
 

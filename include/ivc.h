@@ -59,11 +59,12 @@ int ivc_device_count(void);
 int ivc_set_device(int device);
 /* 1 if the loaded code object matches the current device (gfx950), 0 otherwise */
 int ivc_device_ok(void);
-/* release the library's cached scratch buffers on the current device */
+/* release the library's cached scratch buffers on the current device, and the pinned host
+ * blocks ivc_host_free has cached (process-wide)                                          */
 int ivc_release_scratch(void);
 /* Page-locked host memory for the host-buffer entry points' arrays: a transfer from or to a
  * block of ivc_host_alloc is one DMA (no staging copy); freed blocks are cached by size and
- * reused.  NULL when the runtime cannot pin more memory.                                   */
+ * reused, up to 1 GiB (env IVC_HOST_CACHE_MB overrides; ivc_release_scratch drains it).  NULL when the runtime cannot pin more memory.                                   */
 void* ivc_host_alloc(int64_t bytes);
 int ivc_host_free(void* p);
 /* Store pacing of the fused coefficient encoders (ivc_intra_encode*, ivc_inter_encode*):

@@ -13,12 +13,13 @@ reference's NumPy/SciPy results bit for bit; there is no CPU fallback.
     from ivclab_amd.video import MotionCompensator, VideoCodec
     from ivclab_amd.entropy import ZeroRunCoder
 
-`install_as_ivclab()` registers these modules under the reference's import paths
-(ivclab.signal, ivclab.signal.dct, ...) so unchanged callers pick them up.
+The repository also ships the top-level `ivclab` package (ivclab/), which exposes these
+objects under the reference's import paths (ivclab.signal, ivclab.signal.dct, ...), so the
+reference's callers run unchanged with the repository on PYTHONPATH.
 """
 import importlib
+import os
 import sys
-import types
 
 from .quantization import PatchQuant  # noqa: F401
 from .signal import DiscreteCosineTransform  # noqa: F401
@@ -29,40 +30,22 @@ from .video import MotionCompensator, VideoCodec  # noqa: F401
 
 __version__ = "0.1.0"
 
-_ALIASES = {
-    "ivclab.signal": "ivclab_amd.signal",
-    "ivclab.signal.dct": "ivclab_amd.signal.dct",
-    "ivclab.signal.zigzag": "ivclab_amd.signal.zigzag",
-    "ivclab.signal.color": "ivclab_amd.signal.color",
-    "ivclab.quantization": "ivclab_amd.quantization",
-    "ivclab.quantization.patchquant": "ivclab_amd.quantization.patchquant",
-    "ivclab.utils": "ivclab_amd.utils",
-    "ivclab.utils.shape": "ivclab_amd.utils.shape",
-    "ivclab.utils.metrics": "ivclab_amd.utils.metrics",
-    "ivclab.utils.io": "ivclab_amd.utils.io",
-    "ivclab.video": "ivclab_amd.video",
-    "ivclab.video.motion": "ivclab_amd.video.motion",
-    "ivclab.video.videocodec": "ivclab_amd.video.videocodec",
-    "ivclab.entropy": "ivclab_amd.entropy",
-    "ivclab.entropy.huffman": "ivclab_amd.entropy.huffman",
-    "ivclab.image": "ivclab_amd.image",
-    "ivclab.image.intracodec": "ivclab_amd.image.intracodec",
-    "ivclab.entropy.zerorun": "ivclab_amd.entropy.zerorun",
-}
+_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def install_as_ivclab() -> None:
-    """Make `import ivclab.<hot-path module>` resolve to this package's modules."""
-    root = sys.modules.get("ivclab")
-    if root is None:
-        root = types.ModuleType("ivclab")
-        root.__path__ = []  # namespace-like: only the aliased submodules resolve
-        sys.modules["ivclab"] = root
-    for name, target in _ALIASES.items():
-        mod = importlib.import_module(target)
-        sys.modules[name] = mod
-        parent, _, leaf = name.rpartition(".")
-        setattr(sys.modules[parent], leaf, mod)
-    for cls in (PatchQuant, DiscreteCosineTransform, Patcher, ZigZag, MotionCompensator,
-                ZeroRunCoder, HuffmanCoder, IntraCodec, VideoCodec):
-        setattr(root, cls.__name__, cls)
+def install_as_ivclab():
+    """Import and return the repository's own `ivclab` package (ivclab/ next to this one).
+
+    Callers no longer need this: with the repository on `PYTHONPATH`, `import ivclab...`
+    resolves to that package directly.  It stays for code written against earlier rounds;
+    it puts the repository root on `sys.path` when it is missing, and refuses to proceed
+    when a different `ivclab` (e.g. the reference's) is already imported."""
+    mod = sys.modules.get("ivclab")
+    if mod is None:
+        if _ROOT not in sys.path:
+            sys.path.insert(0, _ROOT)
+        mod = importlib.import_module("ivclab")
+    where = os.path.dirname(os.path.abspath(getattr(mod, "__file__", "") or ""))
+    if os.path.dirname(where) != _ROOT:
+        raise ImportError(f"another 'ivclab' package is already imported from {where}")
+    return mod

@@ -102,13 +102,33 @@ class CopyPool {
 // ivc_host_alloc: page-locked host memory the drop-in classes allocate their NumPy results in
 // (ivclab_amd._native.empty).  A transfer between such a block and the device is one DMA at
 // full PCIe speed with no CPU copy and no first-touch page faults; freed blocks are cached by
-// size (up to kHostCacheMax) so repeated calls of the same shapes reuse them.
+// size (up to host_cache_max(): 1 GiB, or IVC_HOST_CACHE_MB) so repeated calls of the same
+// shapes reuse them; ivc_release_scratch returns the cached blocks to the system.
 std::mutex g_host_mu;
 std::map<uintptr_t, size_t> g_host_live;          // block start -> bytes
 std::multimap<size_t, void*> g_host_cache;        // freed blocks by size
 size_t g_host_cached = 0;
-constexpr size_t kHostCacheMax = 4ull << 30;
 constexpr size_t kHostGrain = 2u << 20;
+
+size_t host_cache_max() {
+  static const size_t v = [] {
+    const char* e = getenv("IVC_HOST_CACHE_MB");
+    if (e && *e) {
+      char* end = nullptr;
+      const long long mb = strtoll(e, &end, 10);
+      if (end && *end == 0 && mb >= 0) return (size_t)mb << 20;
+    }
+    return (size_t)1 << 30;
+  }();
+  return v;
+}
+
+void host_cache_drain() {
+  std::lock_guard<std::mutex> g(g_host_mu);
+  for (auto& kv : g_host_cache) (void)hipHostFree(kv.second);
+  g_host_cache.clear();
+  g_host_cached = 0;
+}
 
 bool host_pinned(const void* p, size_t bytes) {
   std::lock_guard<std::mutex> g(g_host_mu);
@@ -377,7 +397,7 @@ int ivc_host_free(void* p) {
   if (it == g_host_live.end()) return fail(IVC_E_ARG, "ivc_host_free: not a block of ivc_host_alloc");
   const size_t n = it->second;
   g_host_live.erase(it);
-  if (g_host_cached + n <= kHostCacheMax) {
+  if (g_host_cached + n <= host_cache_max()) {
     g_host_cache.emplace(n, p);
     g_host_cached += n;
   } else {
@@ -440,6 +460,7 @@ int ivc_release_scratch(void) {
     c.slot[i] = nullptr;
     c.cap[i] = 0;
   }
+  host_cache_drain();
   return IVC_OK;
 }
 

@@ -872,7 +872,11 @@ __global__ __launch_bounds__(256) void zf_expand_kernel(const int32_t* __restric
         const int cur = valid ? sh[st + j] : 1;
         const int pv = j == 0 ? 1 : sh[st + j - 1];
         const bool rl = valid && pv == 0;
-        const int cc = !valid || rl ? 0 : (cur == 0 ? sh[st + j + 1] : 1);
+        // a run length counts min(run, B + 1): one past B already makes the block overflow,
+        // and the clamp keeps the int32 scan from wrapping on a malformed huge run (a run
+        // <= 0 is flagged by zf_count; clamping it to 0 keeps `pos` inside the row)
+        const int rn = cur == 0 ? min(max(sh[st + j + 1], 0), B + 1) : 1;
+        const int cc = !valid || rl ? 0 : rn;
         const int inc = zf_wave_incl_sum(cc);
         const int pos = carry + inc - cc;
         if (valid && !rl && cur != 0 && pos < B) row[pos] = cur;
@@ -1027,6 +1031,23 @@ int64_t sym_image_scratch_bytes(int64_t n, int64_t ngroups) {
   return bytes;
 }
 
+// test hook, read once per process (see launch_symbols2image)
+static bool s2i_no_fallback() {
+  static const bool v = [] {
+    const char* nf = getenv("IVC_S2I_NO_FALLBACK");
+    return nf && nf[0] == '1';
+  }();
+  return v;
+}
+
+constexpr int64_t IVC_S2I_REJECTED = -100;
+__global__ void s2i_rejected_verdict(const int* ok, int64_t* err) {
+  if (*ok) return;
+  err[0] = IVC_S2I_REJECTED;
+  err[1] = 0;
+  err[2] = 0;
+}
+
 hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, int64_t H,
                                 int64_t W, int C, const QTab& t, int32_t eob, int to_rgb,
                                 double* out, int32_t* coef, void* scratch, int64_t* err,
@@ -1053,10 +1074,12 @@ hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, 
     skip = z.flags + 1;
   }
   // (IVC_S2I_NO_FALLBACK=1, a test hook: the fused kernel's image stands alone, so a test can
-  // tell that it — not the general path — produced the image)
-  const char* nf = getenv("IVC_S2I_NO_FALLBACK");
-  const bool no_fallback = nf && nf[0] == '1';
-  if (skip && no_fallback) return hipSuccess;
+  // tell that it — not the general path — produced the image; when the fused path rejects the
+  // stream, err[0] = IVC_S2I_REJECTED instead of the general decoder's verdict)
+  if (skip && s2i_no_fallback()) {
+    s2i_rejected_verdict<<<1, 1, 0, s>>>(skip, err);
+    return hipGetLastError();
+  }
   e = zr_decode_general(z, sym, n, expected, 64, eob, coef, err, skip, s);
   if (e != hipSuccess) return e;
   return launch_intra_decode_image(coef, nframes, H, W, C, t, 1, to_rgb, out, s, skip);

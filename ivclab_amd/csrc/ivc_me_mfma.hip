@@ -121,7 +121,9 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
       L.raw[k][2] = __builtin_amdgcn_raw_buffer_load_b32(rr, off + 8, 0, 0);
     }
     {
-      const int bx = bx0 + l16;
+      // MFMA row l16 = block pi(l16) = 4 (l16 & 3) + (l16 >> 2): result register i of lane group
+      // g (D row 4g + i) then holds block 4i + g, so a register holds one whole quad of blocks
+      const int bx = bx0 + 4 * (l16 & 3) + (l16 >> 2);
       const int off = bx < w ? (8 * by + 2 * g) * W + 8 * bx : 0x40000000;
       const mf_u32x2 r0 = __builtin_amdgcn_raw_buffer_load_b64(rc, off, 0, 0);
       const mf_u32x2 r1 = __builtin_amdgcn_raw_buffer_load_b64(rc, off + W, 0, 0);
@@ -202,47 +204,17 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
     load(tile + gridDim.x, L);                          // the next tile's inputs, in flight
 
     // ---- search: M-tile outer, dy inner (one new reference row per MFMA) -----------------
+    // M-tile mt (window positions u in [16 mt, 16 mt + 16)) serves blocks [2 mt - 4, 2 mt + 1]:
+    // the quads k - 1 and k for mt in {2k, 2k + 1}.  Iteration k rotates the block operand by
+    // DPP quad_perm so that result register 0 holds quad (k + 3) & 3 (= k - 1) and register 1
+    // quad k: only those two registers are turned into keys (registers 2 and 3 hold quads none
+    // of whose windows are in this M-tile); the C mask kills the quads -1 and 4 (k = 0, 4) and
+    // the non-candidate windows of the live quads.  After iteration k quad k - 1 has seen all
+    // its windows and is reduced; quad k's running key moves to register 0's accumulator.
     const uint32_t* cb = lds + (l16 & 3) * COPY;      // this lane's copy (u & 3 = l16 & 3)
     const int* ev = reinterpret_cast<const int*>(lds + E_OFF) + l16 + dyw0 * U;
-    const int cj = l16 - 32 * g;                      // u - 8j = 16 mt + cj - 8i (block j = 4g+i)
-    int gb0 = INT_MIN, gb1 = INT_MIN, gb2 = INT_MIN, gb3 = INT_MIN;   // per block i: best key
-#pragma unroll 1
-    for (int mt = 0; mt < NMT; ++mt) {
-      const int wd = 4 * mt + (l16 >> 2);             // word of window position u = 16 mt + l16
-      const int v = 16 * mt + cj;
-      const mf_v4i cm = mf_v4i{(unsigned)v <= 32u ? 0 : MASK_C, (unsigned)(v - 8) <= 32u ? 0 : MASK_C,
-                               (unsigned)(v - 16) <= 32u ? 0 : MASK_C,
-                               (unsigned)(v - 24) <= 32u ? 0 : MASK_C};
-      const int* em = ev + 16 * mt;                   // E[dyw0 ..][u]
-      const mf_v4i e0 = mf_v4i{em[0], em[U], em[2 * U], em[3 * U]};
-      const mf_v4i e1 = mf_v4i{em[4 * U], em[5 * U], em[6 * U], em[7 * U]};
-      mf_u32x2 r[10];                                 // rows dyw0 + 2g + k, bytes u .. u+7
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        const int row = dyw0 + 2 * g + k;
-        r[k] = (k < 9 || wave == 3) ? mf_u32x2{cb[row * PITCH + wd], cb[row * PITCH + wd + 1]}
-                                    : mf_u32x2{0u, 0u};
-      }
-      auto step = [&](int dl, uint32_t e) {
-        const mf_v4i aop = mf_v4i{(int)r[dl].x, (int)r[dl].y, (int)r[dl + 1].x, (int)r[dl + 1].y};
-        const mf_v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(bop, aop, cm, 0, 0, 0);
-        gb0 = max(gb0, (int)(((uint32_t)d.x << 8) + e));
-        gb1 = max(gb1, (int)(((uint32_t)d.y << 8) + e));
-        gb2 = max(gb2, (int)(((uint32_t)d.z << 8) + e));
-        gb3 = max(gb3, (int)(((uint32_t)d.w << 8) + e));
-      };
-      step(0, (uint32_t)e0.x);
-      step(1, (uint32_t)e0.y);
-      step(2, (uint32_t)e0.z);
-      step(3, (uint32_t)e0.w);
-      step(4, (uint32_t)e1.x);
-      step(5, (uint32_t)e1.y);
-      step(6, (uint32_t)e1.z);
-      step(7, (uint32_t)e1.w);
-      if (wave == 3) step(8, (uint32_t)em[8 * U]);         // dy = 32: wave 3's ninth
-    }
-    // ---- per block: the best -K' over the 16 lanes of a k-group, then the least raster index
-    // among the lanes holding it (DPP all-reduces within 16-lane rows), then over the waves ----
+    const int cj = l16 - 8 * g;                       // u - 8 (4q + g) = 16 mt + cj - 32 q
+    int* red = reinterpret_cast<int*>(lds + RED_OFF);
     auto dpp_max16 = [](int x) {
       x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0xB1, 0xf, 0xf, false));    // quad_perm 1,0,3,2
       x = max(x, __builtin_amdgcn_update_dpp(INT_MIN, x, 0x4E, 0xf, 0xf, false));    // quad_perm 2,3,0,1
@@ -255,23 +227,72 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
       x = min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x141, 0xf, 0xf, false));
       return min(x, __builtin_amdgcn_update_dpp(INT_MAX, x, 0x140, 0xf, 0xf, false));
     };
-    int* red = reinterpret_cast<int*>(lds + RED_OFF);
-    const int gbs[4] = {gb0, gb1, gb2, gb3};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = gbs[i];
+    // per block: the best -K' over the 16 lanes of a k-group, then the least raster index among
+    // the lanes holding it (DPP all-reduces within 16-lane rows); the waves merge below
+    auto finish = [&](int q, int key) {
       const bool valid = key >= VALID_MIN;
       const int nk = valid ? key >> 7 : INT_MIN;          // -K' (+ a per-block constant)
       const int rank = 127 - (key & 127);
       const int dy = dyw0 + rank / 10;
       const int u = 16 * (rank % 10) + l16;
-      const int ri = dy * N + u - 8 * (4 * g + i);        // raster index dy * 33 + dx
+      const int blk = 4 * q + g;
+      const int ri = dy * N + u - 8 * blk;                // raster index dy * 33 + dx
       const int best = dpp_max16(nk);
       const int bri = dpp_min16(valid && nk == best ? ri : INT_MAX);
       if (l16 == 0) {
-        red[2 * (wave * TB + 4 * g + i)] = best;
-        red[2 * (wave * TB + 4 * g + i) + 1] = bri;
+        red[2 * (wave * TB + blk)] = best;
+        red[2 * (wave * TB + blk) + 1] = bri;
       }
+    };
+    // quad_perm rotations of the block operand: lane i of a quad takes lane (i + r) & 3's
+    auto rot = [](const mf_v4i& x, auto ctrl) {
+      constexpr int c = decltype(ctrl)::value;
+      return mf_v4i{__builtin_amdgcn_mov_dpp(x.x, c, 0xf, 0xf, false),
+                    __builtin_amdgcn_mov_dpp(x.y, c, 0xf, 0xf, false),
+                    __builtin_amdgcn_mov_dpp(x.z, c, 0xf, 0xf, false),
+                    __builtin_amdgcn_mov_dpp(x.w, c, 0xf, 0xf, false)};
+    };
+    mf_v4i bk = rot(bop, std::integral_constant<int, 0x93>{});   // r = 3: quads 3, 0, 1, 2
+    int acc0 = INT_MIN, acc1 = INT_MIN;                 // running best key of quads k - 1, k
+#pragma unroll 1
+    for (int k = 0; k < NMT / 2; ++k) {
+      const int q0 = (k + 3) & 3, q1 = k & 3;
+#pragma unroll
+      for (int hm = 0; hm < 2; ++hm) {
+        const int mt = 2 * k + hm;
+        const int wd = 4 * mt + (l16 >> 2);             // word of window position u = 16 mt + l16
+        const int v0 = 16 * mt + cj - 32 * q0, v1 = 16 * mt + cj - 32 * q1;
+        const mf_v4i cm = mf_v4i{(unsigned)v0 <= 32u ? 0 : MASK_C, (unsigned)v1 <= 32u ? 0 : MASK_C, 0, 0};
+        const int* em = ev + 16 * mt;                   // E[dyw0 ..][u]
+        const mf_v4i e0 = mf_v4i{em[0], em[U], em[2 * U], em[3 * U]};
+        const mf_v4i e1 = mf_v4i{em[4 * U], em[5 * U], em[6 * U], em[7 * U]};
+        mf_u32x2 r[10];                                 // rows dyw0 + 2g + k, bytes u .. u+7
+#pragma unroll
+        for (int kk = 0; kk < 10; ++kk) {
+          const int row = dyw0 + 2 * g + kk;
+          r[kk] = (kk < 9 || wave == 3) ? mf_u32x2{cb[row * PITCH + wd], cb[row * PITCH + wd + 1]}
+                                        : mf_u32x2{0u, 0u};
+        }
+        auto step = [&](int dl, uint32_t e) {
+          const mf_v4i aop = mf_v4i{(int)r[dl].x, (int)r[dl].y, (int)r[dl + 1].x, (int)r[dl + 1].y};
+          const mf_v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(bk, aop, cm, 0, 0, 0);
+          acc0 = max(acc0, (int)(((uint32_t)d.x << 8) + e));
+          acc1 = max(acc1, (int)(((uint32_t)d.y << 8) + e));
+        };
+        step(0, (uint32_t)e0.x);
+        step(1, (uint32_t)e0.y);
+        step(2, (uint32_t)e0.z);
+        step(3, (uint32_t)e0.w);
+        step(4, (uint32_t)e1.x);
+        step(5, (uint32_t)e1.y);
+        step(6, (uint32_t)e1.z);
+        step(7, (uint32_t)e1.w);
+        if (wave == 3) step(8, (uint32_t)em[8 * U]);         // dy = 32: wave 3's ninth
+      }
+      if (k > 0) finish(q0, acc0);                      // quad k - 1 is complete
+      acc0 = acc1;
+      acc1 = INT_MIN;
+      bk = rot(bk, std::integral_constant<int, 0x39>{});  // r + 1: quad_perm 1,2,3,0
     }
     __syncthreads();
     if (tid < TB) {

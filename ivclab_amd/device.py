@@ -207,6 +207,12 @@ def symbols2image(sym, C, table, out, err, eob=4000, to_rgb=False, stream=None):
     _contig(sym, "sym"); _contig(out, "out"); _contig(err, "err")
     if sym.dtype != torch.int32 or out.dtype != torch.float64 or err.dtype != torch.int64:
         raise ValueError("symbols2image: int32 sym, float64 out, int64 err")
+    if sym.dim() != 1 or err.dim() != 1 or err.numel() < 3:
+        raise ValueError("symbols2image: sym must be 1-D, err must hold 3 values")
+    if out.dim() != 4 or out.shape[3] != 3 or out.shape[1] % 8 or out.shape[2] % 8:
+        raise ValueError("symbols2image: out must be [F, 8h, 8w, 3] (the kernel writes 3 planes)")
+    if int(C) not in (1, 3):
+        raise ValueError("symbols2image: C must be 1 or 3")
     F, H, W, _ = out.shape
     t = N.table_arg(table)
     N.check(N.lib().ivc_symbols2image_dev(sym.data_ptr(), sym.numel(), F, H, W, int(C), N.ptr(t),

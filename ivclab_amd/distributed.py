@@ -36,13 +36,36 @@ def _host_staged(t, group=None):
     return t.is_cuda and dist.get_backend(group) == "gloo"
 
 
-def global_bounds(local_mm, group=None):
+def init_single_rank(device, port=None):
+    """A one-rank process group on `device` (backend "nccl" = RCCL): the collectives below then
+    run through RCCL even without a second GPU (`force=True`), so the exchange's RCCL path is
+    exercised on a one-GPU box.  Rendezvous on 127.0.0.1."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    if port is None:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0,
+                            world_size=1, device_id=torch.device(device))
+    return dist
+
+
+def _collective(group, force):
+    import torch.distributed as dist
+    return dist.is_initialized() and (force or dist.get_world_size(group) > 1)
+
+
+def global_bounds(local_mm, group=None, force=False):
     """(min, max) over every rank of the int32 pairs local_mm = [min, max] (device tensor,
-    ivc_minmax_i32's output) with one all-reduce (MAX of [-min, max] in int64)."""
+    ivc_minmax_i32's output) with one all-reduce (MAX of [-min, max] in int64).  With one
+    rank the all-reduce is skipped unless `force`."""
     import torch
     import torch.distributed as dist
     v = torch.stack([-local_mm[0].to(torch.int64), local_mm[1].to(torch.int64)])
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _collective(group, force):
         if _host_staged(v, group):
             v = v.cpu()
         dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
@@ -50,16 +73,17 @@ def global_bounds(local_mm, group=None):
     return -lo, hi
 
 
-def global_histogram(local_hist, group=None):
+def global_histogram(local_hist, group=None, force=False):
     """Sum of every rank's histogram (a 1-D int64 tensor on this rank's device) via one
-    all-gather; every rank receives the same result."""
+    all-gather; every rank receives the same result.  With one rank the all-gather is
+    skipped (a copy is returned) unless `force`."""
     import torch
     import torch.distributed as dist
-    if not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not _collective(group, force):
         return local_hist.clone()
     world = dist.get_world_size(group)
     if _host_staged(local_hist, group):
-        return global_histogram(local_hist.cpu(), group).to(local_hist.device)
+        return global_histogram(local_hist.cpu(), group, force).to(local_hist.device)
     gathered = torch.empty((world,) + tuple(local_hist.shape), dtype=local_hist.dtype,
                            device=local_hist.device)
     try:

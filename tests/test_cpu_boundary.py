@@ -117,7 +117,9 @@ def test_install_as_ivclab():
     import sys
 
     import ivclab_amd as IA
-    IA.install_as_ivclab()
+    for k in [k for k in sys.modules if k == "ivclab" or k.startswith("ivclab.")]:
+        del sys.modules[k]
+    assert IA.install_as_ivclab() is sys.modules["ivclab"]
     try:
         from ivclab.quantization import PatchQuant
         from ivclab.signal import DiscreteCosineTransform

@@ -1,11 +1,12 @@
-"""The drop-in boundary seen from the reference's own callers: under
-`ivclab_amd.install_as_ivclab()` the import lines of the reference's tests and chapter 3/4
-exercises resolve unchanged, and tests/ch3.py's assertions (tests/ch3.py:18-47) hold on a
-committed synthetic stand-in for the absent data/satpic1.bmp with the thresholds the
-reference itself computes on that image (tests/golden/ch3.npz, make_golden.py make_ch3).
+"""The drop-in boundary seen from the reference's own callers: with only this repository on
+PYTHONPATH (no prelude, no install step, a scratch working directory) the import lines of
+the reference's tests and chapter 3/4 exercises resolve unchanged to the repository's own
+`ivclab` package, and tests/ch3.py's assertions (tests/ch3.py:18-47) hold on a committed
+synthetic stand-in for the absent data/satpic1.bmp with the thresholds the reference itself
+computes on that image (tests/golden/ch3.npz, make_golden.py make_ch3).
 
-The import checks run in a fresh interpreter (install_as_ivclab edits sys.modules) and need
-no GPU: importing the drop-in loads libivc lazily.  The ch3 assertions compute on the GPU."""
+The import checks run in a fresh interpreter and need no GPU: importing the drop-in loads
+libivc lazily.  The ch3 assertions compute on the GPU."""
 import ast
 import glob
 import os
@@ -32,17 +33,67 @@ from ivclab.utils.metrics import calc_mse
 """
 
 
-def run_py(code):
-    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
-                       timeout=300)
+def caller_env():
+    """The caller's environment: PYTHONPATH = this repository and nothing else of ours."""
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT
+    return env
+
+
+def run_py(code, cwd=None):
+    """Run `code` as an unchanged caller would: a fresh interpreter, the repository only on
+    PYTHONPATH, started from a directory outside it."""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        r = subprocess.run([sys.executable, "-c", code], cwd=cwd or d, env=caller_env(),
+                           capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     return r.stdout
 
 
 def test_ch3_import_block_resolves():
-    out = run_py("import ivclab_amd; ivclab_amd.install_as_ivclab()\n" + CH3_IMPORTS +
-                 "print(imread.__module__, Patcher.__module__, calc_mse.__module__)")
-    assert out.split() == ["ivclab_amd.utils.io", "ivclab_amd.utils.shape", "ivclab_amd.utils.metrics"]
+    out = run_py(CH3_IMPORTS + "import ivclab, os\n"
+                 "print(imread.__module__, Patcher.__module__, calc_mse.__module__)\n"
+                 "print(os.path.dirname(os.path.dirname(ivclab.__file__)))")
+    lines = out.splitlines()
+    assert lines[0].split() == ["ivclab_amd.utils.io", "ivclab_amd.utils.shape",
+                                "ivclab_amd.utils.metrics"]
+    assert lines[1] == ROOT
+
+
+def test_package_layout_mirrors_reference():
+    """ivclab/__init__.py:1-5 star-imports entropy, image, quantization, utils, video (not
+    signal); the subpackages export the hot-path names; `import ivclab` needs no
+    constriction; names outside the hot path raise ImportError."""
+    out = run_py("""
+import sys, ivclab
+assert 'constriction' not in sys.modules
+for n in ('PatchQuant', 'ZigZag', 'Patcher', 'imread', 'calc_psnr', 'calc_mse', 'IntraCodec',
+          'MotionCompensator', 'VideoCodec', 'HuffmanCoder', 'ZeroRunCoder', 'stats_marg',
+          'smooth_pmf', 'calc_entropy', 'min_code_length'):
+    assert hasattr(ivclab, n), n
+assert not hasattr(ivclab, 'DiscreteCosineTransform')   # signal is not star-imported
+import ivclab.signal.zigzag, ivclab.utils.shape, ivclab.video.motion, ivclab.entropy.entropy
+assert ivclab.signal.zigzag.zigzag_scan.__module__ == 'ivclab_amd.signal.zigzag'
+assert not hasattr(ivclab.signal, 'zigzag_scan')       # signal/__init__.py does not export it
+import ivclab_amd
+assert ivclab.signal.DiscreteCosineTransform is ivclab_amd.DiscreteCosineTransform
+assert ivclab.video.videocodec.VideoCodec is ivclab_amd.VideoCodec
+for mod, name in (('ivclab.signal', 'downsample'), ('ivclab.signal', 'FilterPipeline'),
+                  ('ivclab.image', 'IntraCodecAdaptive'), ('ivclab.entropy', 'stats_joint')):
+    try:
+        exec(f'from {mod} import {name}')
+    except ImportError:
+        pass
+    else:
+        raise AssertionError(name)
+try:
+    ivclab.signal.downsample
+except AttributeError as e:
+    assert 'outside the MI355X block-codec hot path' in str(e)
+print('ok')
+""")
+    assert out.strip() == "ok"
 
 
 def _reference_import_lines():
@@ -68,7 +119,7 @@ def _reference_import_lines():
 def test_reference_callers_import_lines_resolve():
     stmts = _reference_import_lines()
     assert len(stmts) >= 10
-    code = "import ivclab_amd; ivclab_amd.install_as_ivclab()\n" + "\n".join(stmts) + "\nprint('ok')"
+    code = "\n".join(stmts) + "\nprint('ok')"
     assert run_py(code).strip() == "ok"
 
 
@@ -87,7 +138,7 @@ def test_ch3_assertions_on_standin(golden):
     """tests/ch3.py:18-47 through the drop-in names, on the stand-in image: the same
     assertions and deltas, with the expected values the reference computes for this image
     (and, tighter, equal to them: the path is bit-exact)."""
-    code = "import ivclab_amd; ivclab_amd.install_as_ivclab()\n" + CH3_IMPORTS + f"""
+    code = CH3_IMPORTS + f"""
 import json
 orig_img = imread({STANDIN!r})
 patcher = Patcher(window_size=(8, 8))
@@ -123,7 +174,6 @@ RD_SCALES = [0.05, 0.1, 0.15, 0.2, 0.3]
 RD_CODE = """
 import json
 import numpy as np
-import ivclab_amd; ivclab_amd.install_as_ivclab()
 from ivclab.image import IntraCodec
 from ivclab.utils import calc_psnr
 rng = np.random.default_rng(31)

@@ -2,8 +2,8 @@
 working P-frame path) through the drop-in, against the same loop built from oracle
 primitives (tests/closed_loop.py restates the loop once; both runs use it).
 
-The drop-in run happens in a fresh interpreter under `ivclab_amd.install_as_ivclab()` with
-the exercise's own import block (ex1.py:1-6), so every primitive is resolved by the names
+The drop-in run happens in a fresh interpreter with only the repository on PYTHONPATH (no
+prelude) and the exercise's own import block (ex1.py:1-6), so every primitive is resolved by the names
 the exercise uses: IntraCodec (GPU DCT / quantiser / zig-zag / zero-run, host Huffman),
 MotionCompensator (GPU float64 NumPy-semantics search and block copy), rgb2ycbcr /
 ycbcr2rgb (GPU colour kernels), stats_marg (GPU histogram), HuffmanCoder.  Every frame's
@@ -33,7 +33,6 @@ SR = 4                       # the exercise's search range (ex1.py:392)
 DROPIN = """
 import json, sys
 import numpy as np
-import ivclab_amd; ivclab_amd.install_as_ivclab()
 from ivclab.image import IntraCodec
 from ivclab.entropy import HuffmanCoder, stats_marg
 from ivclab.signal import rgb2ycbcr, ycbcr2rgb
@@ -120,8 +119,8 @@ def test_ch4_closed_loop_through_dropin(tmp_path):
     code = f"OUT = {str(tmp_path)!r}\n" + DROPIN.format(tests=os.path.join(ROOT, "tests"),
                                                          frames=str(tmp_path / "frames.npy"),
                                                          scales=SCALES, sr=SR)
-    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True,
-                       timeout=600)
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(tmp_path), capture_output=True,
+                       text=True, timeout=600, env=dict(os.environ, PYTHONPATH=ROOT))
     assert r.returncode == 0, r.stderr[-3000:]
     summary = json.loads(r.stdout.strip().splitlines()[-1])
     assert len(summary) == len(SCALES) * len(frames)

@@ -786,6 +786,20 @@ def test_zerorun_decode_fast_path_boundaries():
         "too_few": sym[: np.flatnonzero(sym == 4000)[nb // 2]],
         "ends_after_zero": np.concatenate([sym[: np.flatnonzero(sym == 4000)[10] + 1], [5, 0]]),
     }
+    k10 = int(np.flatnonzero(sym == 4000)[10]) + 1          # a block boundary
+    # huge runs: the reference extends the block by the run and raises at once;
+    # the fast path must neither wrap its int32 run-length scan nor write outside its row.
+    # Expected errors written out (the oracle would materialise a 2^31-element list)
+    huge = {
+        "huge_run": (np.concatenate([[0, 2**31 - 1, 5, 4000], sym]), 2**31 - 1),
+        "wrapping_runs": (np.concatenate([[0, 2**30, 0, 2**30, 5, 4000], sym]), 2**30),
+        "late_huge_run": (np.concatenate([sym[:k10], [7, 0, 2**31 - 1, 4000], sym[k10:]]), 2**31),
+    }
+    for name, (s, n_exceeded) in huge.items():
+        s = np.ascontiguousarray(s, np.int32)
+        with pytest.raises(ValueError) as got:
+            Z.decode(s, shape)
+        assert str(got.value) == f"Block size exceeded: {n_exceeded}", name
     for name, s in bad.items():
         s = np.ascontiguousarray(s, np.int32)
         try:
