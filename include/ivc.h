@@ -59,6 +59,11 @@ int ivc_device_count(void);
 int ivc_set_device(int device);
 /* 1 if the loaded code object matches the current device (gfx950), 0 otherwise */
 int ivc_device_ok(void);
+/* Host-buffer calls whose output is in page-locked memory (ivc_host_alloc) move their data in
+ * chunks of chunk_bytes (the larger of input and output per chunk; default 8 MiB) that go
+ * upload -> kernel -> download on 3 streams, overlapping one chunk's copies with another's;
+ * 0 runs every call in one piece.  Process-wide.                                          */
+int ivc_set_host_pipeline(int64_t chunk_bytes);
 /* release the library's cached scratch buffers on the current device, and the pinned host
  * blocks ivc_host_free has cached (process-wide)                                          */
 int ivc_release_scratch(void);
@@ -114,6 +119,15 @@ int ivc_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_
                int inverse, int norm);
 int ivc_dct8x8_dev(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
                    int inverse, int norm, void* stream);
+/* The same transform of the blocks of Patcher.patch's view of a C-contiguous [H, W, C] image
+ * (H, W multiples of 8), read in place: dst = [H/8, W/8, C, 8, 8], i.e.
+ * transform(patch(img)) without gathering the strided view first.
+ * Replaces: DiscreteCosineTransform.transform on Patcher.patch
+ *           ivclab/signal/dct.py:12-28 + ivclab/utils/shape.py:45-54                      */
+int ivc_dct8x8_image(const void* img, int src_dtype, int64_t H, int64_t W, int64_t C, void* dst,
+                     int dst_dtype, int inverse, int norm);
+int ivc_dct8x8_image_dev(const void* img, int src_dtype, int64_t H, int64_t W, int64_t C,
+                         void* dst, int dst_dtype, int inverse, int norm, void* stream);
 
 /* ---------------------------------------------------------------- quantization ----- */
 /* src: nblk x C x 64 (C = 1 or 3; C = 1 broadcasts over the 3 table planes), table: the

@@ -55,6 +55,9 @@ _SIGS = {
     "ivc_histogram_occupancy": ([], _I),
     "ivc_dct8x8": ([_P, _I, _L, _P, _I, _I, _I], _I),
     "ivc_dct8x8_dev": ([_P, _I, _L, _P, _I, _I, _I, _P], _I),
+    "ivc_dct8x8_image": ([_P, _I, _L, _L, _L, _P, _I, _I, _I], _I),
+    "ivc_set_host_pipeline": ([_L], _I),
+    "ivc_dct8x8_image_dev": ([_P, _I, _L, _L, _L, _P, _I, _I, _I, _P], _I),
     "ivc_quantize": ([_P, _I, _L, _I, _P, _I, _P], _I),
     "ivc_quantize_dev": ([_P, _I, _L, _I, _P, _I, _P, _P], _I),
     "ivc_dequantize": ([_P, _I, _L, _I, _P, _I, _P], _I),

@@ -9,6 +9,7 @@
 #include <condition_variable>
 #include <functional>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -145,9 +146,18 @@ constexpr int kSlots = 6;
 constexpr int kPinSlots = 4;
 constexpr size_t kPinChunk = 8u << 20;      // bytes per pinned slot
 constexpr size_t kPinMin = 1u << 20;        // smaller transfers go straight from pageable memory
+constexpr int kAux = 3;                     // pipelined host-buffer calls: streams
+constexpr size_t kPipeMin = 4u << 20;       // smaller outputs go in one piece
+// bytes per pipelined chunk (the larger of in / out); 0 = no pipelining (ivc_set_host_pipeline)
+std::atomic<size_t> g_pipe_chunk{8u << 20};
 struct DevCtx {
   std::mutex mu;
   hipStream_t stream = nullptr;
+  hipStream_t aux[kAux] = {};
+  hipEvent_t aux_ev = nullptr;              // the main stream's upload, for the aux streams
+  int aux_state = 0;                        // 0 untried, 1 ready, -1 unavailable
+  void* tiny = nullptr;                     // page-locked, device-mapped block for tiny calls
+  int tiny_state = 0;                       // 0 untried, 1 ready, -1 unavailable
   void* slot[kSlots] = {};
   size_t cap[kSlots] = {};
   void* pin[kPinSlots] = {};
@@ -156,6 +166,27 @@ struct DevCtx {
   int pin_next = 0;
 };
 DevCtx g_ctx[kMaxDev];
+
+bool aux_ready(DevCtx* c) {
+  if (c->aux_state == 0) {
+    c->aux_state = 1;
+    for (int i = 0; i < kAux && c->aux_state == 1; ++i)
+      if (hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking) != hipSuccess) c->aux_state = -1;
+    if (c->aux_state == 1 && hipEventCreateWithFlags(&c->aux_ev, hipEventDisableTiming) != hipSuccess)
+      c->aux_state = -1;
+    (void)hipGetLastError();
+  }
+  return c->aux_state == 1;
+}
+
+constexpr size_t kTinyMax = 64u << 10;      // bytes of input and of output for a tiny call
+bool tiny_ready(DevCtx* c) {
+  if (c->tiny_state == 0) {
+    c->tiny_state = hipHostMalloc(&c->tiny, 2 * kTinyMax, hipHostMallocDefault) == hipSuccess ? 1 : -1;
+    (void)hipGetLastError();
+  }
+  return c->tiny_state == 1;
+}
 
 bool pinned_ready(DevCtx* c) {
   if (c->pin_state == 0) {
@@ -281,9 +312,75 @@ struct Staging {
     }
     return status;
   }
-  int sync() {
-    if (status) return status;
+  // A unit-separable op (DCT blocks, quantiser blocks, zig-zag rows, block rows of an image)
+  // from `src` to the page-locked `dst` (the drop-in's own result arrays, ivc_host_alloc):
+  // chunks of units go upload -> kernel -> download round-robin on kAux streams, so one
+  // chunk's upload, another's kernel and a third's download overlap (the PCIe link is full
+  // duplex).  A page-locked `src` is uploaded chunk by chunk; a pageable one whole, through the
+  // staging ring on the main stream, which the aux streams then wait for.  Returns false, with
+  // nothing enqueued, when it does not apply (a small or pageable output): the caller then
+  // runs the op in one piece.  launch(d_in, d_out, units, stream) -> hipError_t.
+  template <typename L>
+  bool pipelined(const void* src, size_t ib, void* dst, size_t ob, int64_t n, const char* what,
+                 L&& launch) {
+    if (status || n <= 0) return false;
+    const size_t IB = ib * (size_t)n, OB = ob * (size_t)n;
+    const size_t chunk = g_pipe_chunk.load(std::memory_order_relaxed);
+    if (chunk == 0 || OB < kPipeMin || !host_pinned(dst, OB) || !aux_ready(ctx)) return false;
+    const bool in_pinned = host_pinned(src, IB);
+    char* d_in = (char*)(in_pinned ? alloc(IB) : in(src, IB));
+    char* d_out = (char*)alloc(OB);
+    if (status) return true;
+    if (!in_pinned) {
+      hipError_t e = hipEventRecord(ctx->aux_ev, ctx->stream);
+      for (int i = 0; i < kAux && e == hipSuccess; ++i) e = hipStreamWaitEvent(ctx->aux[i], ctx->aux_ev, 0);
+      if (e != hipSuccess) { status = fail_hip(e, "hipStreamWaitEvent"); return true; }
+    }
+    const size_t big = ib > ob ? ib : ob;
+    const int64_t per = (int64_t)(chunk / big > 0 ? chunk / big : 1);
+    aux_used = true;
+    for (int64_t u0 = 0, k = 0; u0 < n && !status; u0 += per, ++k) {
+      hipStream_t s = ctx->aux[k % kAux];
+      const int64_t nu = per < n - u0 ? per : n - u0;
+      hipError_t e = hipSuccess;
+      if (in_pinned)
+        e = hipMemcpyAsync(d_in + u0 * ib, (const char*)src + u0 * ib, nu * ib, hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) { status = fail_hip(e, "hipMemcpyAsync H2D"); break; }
+      e = launch(d_in + u0 * ib, d_out + u0 * ob, nu, s);
+      if (launched(e, what)) break;
+      e = hipMemcpyAsync((char*)dst + u0 * ob, d_out + u0 * ob, nu * ob, hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) status = fail_hip(e, "hipMemcpyAsync D2H");
+    }
+    return true;
+  }
+  bool aux_used = false;
+  // A tiny call (one 8x8 block, a (3, 8, 8) stack: the reference's per-block loops,
+  // exercises/ch3/E3-1_claude.py:47-60): the input is copied into a page-locked block the
+  // device addresses directly, the kernel reads it and writes its output there over the bus
+  // (no DMA transfers to set up), then one sync and a copy out: one launch per call.
+  // Returns false, nothing done, when the sizes do not qualify.
+  template <typename L>
+  bool tiny(const void* src, size_t IB, void* dst, size_t OB, const char* what, L&& launch) {
+    if (status || IB > kTinyMax || OB > kTinyMax || !tiny_ready(ctx)) return false;
+    char* ti = (char*)ctx->tiny;
+    char* to = ti + kTinyMax;
+    if (IB) memcpy(ti, src, IB);
+    if (launched(launch(ti, to, ctx->stream), what)) return true;
     hipError_t e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) { status = fail_hip(e, "hipStreamSynchronize"); return true; }
+    if (OB) memcpy(dst, to, OB);
+    return true;
+  }
+  int sync() {
+    hipError_t e = hipSuccess;
+    if (aux_used)
+      for (int i = 0; i < kAux; ++i) {
+        hipError_t ei = hipStreamSynchronize(ctx->aux[i]);
+        if (e == hipSuccess) e = ei;
+      }
+    if (status) return status;
+    hipError_t em = hipStreamSynchronize(ctx->stream);
+    if (e == hipSuccess) e = em;
     if (e != hipSuccess) return status = fail_hip(e, "hipStreamSynchronize");
     return IVC_OK;
   }
@@ -406,6 +503,12 @@ int ivc_host_free(void* p) {
   return IVC_OK;
 }
 
+int ivc_set_host_pipeline(int64_t chunk_bytes) {
+  if (chunk_bytes < 0) return fail(IVC_E_ARG, "ivc_set_host_pipeline: chunk must be >= 0");
+  g_pipe_chunk.store((size_t)chunk_bytes, std::memory_order_relaxed);
+  return IVC_OK;
+}
+
 int ivc_set_store_pace(double total_gbps) {
   if (!(total_gbps >= 0)) return fail(IVC_E_ARG, "ivc_set_store_pace: rate must be >= 0");
   set_store_pace_gbps(total_gbps);
@@ -481,12 +584,53 @@ int ivc_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_
   TRY(st.open());
   const size_t ib = (size_t)nblk * 64 * dtype_size(src_dtype);
   const size_t ob = (size_t)nblk * 64 * dtype_size(dst_dtype);
+  if (st.tiny(src, ib, dst, ob, "dct8x8", [&](const void* i, void* o, hipStream_t s) {
+        return launch_dct8x8(i, src_dtype, nblk, o, dst_dtype, inverse, norm, s);
+      }))
+    return st.status;
+  if (st.pipelined(src, 64 * dtype_size(src_dtype), dst, 64 * dtype_size(dst_dtype), nblk, "dct8x8",
+                   [&](const void* i, void* o, int64_t n, hipStream_t s) {
+                     return launch_dct8x8(i, src_dtype, n, o, dst_dtype, inverse, norm, s);
+                   }))
+    return st.sync();
   void* d_in = st.in(src, ib);
   void* d_out = st.alloc(ob);
   if (st.status) return st.status;
   TRY(st.launched(launch_dct8x8(d_in, src_dtype, nblk, d_out, dst_dtype, inverse, norm,
                                 st.ctx->stream), "dct8x8"));
   TRY(st.out(dst, d_out, ob));
+  return st.sync();
+}
+
+int ivc_dct8x8_image_dev(const void* img, int src_dtype, int64_t H, int64_t W, int64_t C, void* dst,
+                         int dst_dtype, int inverse, int norm, void* stream) {
+  TRY(check_dct(src_dtype, 0, dst_dtype, norm));
+  TRY(check_frames(1, H, W, "dct8x8_image"));
+  CHECK(C >= 1 && C <= 4096, IVC_E_SHAPE, "dct8x8_image: C must be in [1, 4096]");
+  return dev_launch(launch_dct8x8_image(img, src_dtype, H / 8, W, C, dst, dst_dtype, inverse, norm,
+                                        (hipStream_t)stream), "dct8x8_image");
+}
+
+int ivc_dct8x8_image(const void* img, int src_dtype, int64_t H, int64_t W, int64_t C, void* dst,
+                     int dst_dtype, int inverse, int norm) {
+  TRY(check_dct(src_dtype, 0, dst_dtype, norm));
+  TRY(check_frames(1, H, W, "dct8x8_image"));
+  CHECK(C >= 1 && C <= 4096, IVC_E_SHAPE, "dct8x8_image: C must be in [1, 4096]");
+  const int64_t rows = H / 8;
+  if (rows == 0 || W == 0) return IVC_OK;
+  Staging st;
+  TRY(st.open());
+  const size_t rib = (size_t)(8 * W * C) * dtype_size(src_dtype);          // per block row
+  const size_t rob = (size_t)(W / 8 * C) * 64 * dtype_size(dst_dtype);
+  auto go = [&](const void* i, void* o, int64_t n, hipStream_t s) {
+    return launch_dct8x8_image(i, src_dtype, n, W, C, o, dst_dtype, inverse, norm, s);
+  };
+  if (st.pipelined(img, rib, dst, rob, rows, "dct8x8_image", go)) return st.sync();
+  void* d_in = st.in(img, rib * rows);
+  void* d_out = st.alloc(rob * rows);
+  if (st.status) return st.status;
+  TRY(st.launched(go(d_in, d_out, rows, st.ctx->stream), "dct8x8_image"));
+  TRY(st.out(dst, d_out, rob * rows));
   return st.sync();
 }
 
@@ -510,6 +654,15 @@ int ivc_quantize(const void* src, int src_dtype, int64_t nblk, int C, const doub
   Staging st;
   TRY(st.open());
   const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
+  if (st.tiny(src, ib, dst, ob, "quantize", [&](const void* i, void* o, hipStream_t s) {
+        return launch_quantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s);
+      }))
+    return st.status;
+  if (st.pipelined(src, (size_t)C * 64 * dtype_size(src_dtype), dst, 192 * 4, nblk, "quantize",
+                   [&](const void* i, void* o, int64_t n, hipStream_t s) {
+                     return launch_quantize(i, src_dtype, n, C, t, calc_dtype, (int32_t*)o, s);
+                   }))
+    return st.sync();
   void* d_in = st.in(src, ib);
   int32_t* d_out = (int32_t*)st.alloc(ob);
   if (st.status) return st.status;
@@ -538,6 +691,15 @@ int ivc_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const do
   Staging st;
   TRY(st.open());
   const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
+  if (st.tiny(src, ib, dst, ob, "dequantize", [&](const void* i, void* o, hipStream_t s) {
+        return launch_dequantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s);
+      }))
+    return st.status;
+  if (st.pipelined(src, (size_t)C * 64 * dtype_size(src_dtype), dst, 192 * 4, nblk, "dequantize",
+                   [&](const void* i, void* o, int64_t n, hipStream_t s) {
+                     return launch_dequantize(i, src_dtype, n, C, t, calc_dtype, (int32_t*)o, s);
+                   }))
+    return st.sync();
   void* d_in = st.in(src, ib);
   int32_t* d_out = (int32_t*)st.alloc(ob);
   if (st.status) return st.status;
@@ -564,6 +726,15 @@ int ivc_zigzag(const void* src, int64_t nrow, int64_t stride, int esize, int inv
   Staging st;
   TRY(st.open());
   const size_t ib = (size_t)nrow * stride * esize, ob = (size_t)nrow * 64 * esize;
+  if (st.tiny(src, ib, dst, ob, "zigzag", [&](const void* i, void* o, hipStream_t s) {
+        return launch_zigzag(i, nrow, stride, esize, inverse, o, s);
+      }))
+    return st.status;
+  if (st.pipelined(src, (size_t)stride * esize, dst, 64 * (size_t)esize, nrow, "zigzag",
+                   [&](const void* i, void* o, int64_t n, hipStream_t s) {
+                     return launch_zigzag(i, n, stride, esize, inverse, o, s);
+                   }))
+    return st.sync();
   void* d_in = st.in(src, ib);
   void* d_out = st.alloc(ob);
   if (st.status) return st.status;
@@ -604,6 +775,18 @@ int ivc_intra_encode(const void* img, int dtype, int64_t nframes, int64_t H, int
   TRY(st.open());
   const size_t ib = (size_t)(nframes * H * W * C) * dtype_size(dtype);
   const size_t ob = (size_t)(nframes * (H / 8) * (W / 8)) * 192 * 4;
+  // pipelined by frames, or by block rows of a single frame
+  const bool by_rows = nframes == 1;
+  const int64_t units = by_rows ? H / 8 : nframes;
+  const size_t uib = ib / (size_t)units, uob = ob / (size_t)units;
+  if (st.pipelined(img, uib, out, uob, units, "intra_encode",
+                   [&](const void* i, void* o, int64_t n, hipStream_t s) {
+                     return by_rows ? launch_intra_encode(i, dtype, 1, 8 * n, W, C, t, calc_dtype, zigzag,
+                                                          (int32_t*)o, s)
+                                    : launch_intra_encode(i, dtype, n, H, W, C, t, calc_dtype, zigzag,
+                                                          (int32_t*)o, s);
+                   }))
+    return st.sync();
   void* d_in = st.in(img, ib);
   int32_t* d_out = (int32_t*)st.alloc(ob);
   if (st.status) return st.status;

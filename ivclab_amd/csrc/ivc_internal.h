@@ -26,6 +26,8 @@ bool dtype_is_float(int dtype);
 // all launchers enqueue on `s` and return hipSuccess / the launch error
 hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
                          int inverse, int norm, hipStream_t s);
+hipError_t launch_dct8x8_image(const void* img, int src_dtype, int64_t rows, int64_t W, int64_t C,
+                               void* dst, int dst_dtype, int inverse, int norm, hipStream_t s);
 hipError_t launch_quantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
                            int calc_dtype, int32_t* dst, hipStream_t s);
 hipError_t launch_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,

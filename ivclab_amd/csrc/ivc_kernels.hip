@@ -96,9 +96,17 @@ __device__ __forceinline__ void load8(const TI* __restrict__ p, TI* v) {
 // Standalone 2-D DCT-II / DCT-III of contiguous 8x8 units (dct.py:12-46).  (The decode chain
 // dequantise -> DCT-III has its own kernel: ivc_decode.hip.)
 // ======================================================================================
-template <typename TI, typename T, bool INV>
+// IMG: the units are the blocks of Patcher.patch's view of an [H, W, C] image
+// (shape.py:45-54: unit (by, bx, c) row r = image row 8 by + r, columns 8 bx .., channel c),
+// read in place — the view is never gathered on the host; the output is the view's
+// [H/8, W/8, C, 8, 8] layout
+struct ImgLayout {
+  int64_t W, C, per_row;    // image width, channels, units per block row (W / 8 * C)
+};
+template <typename TI, typename T, bool INV, bool IMG = false>
 __global__ __launch_bounds__(256) void dct8x8_kernel(const TI* __restrict__ src, int64_t nunit,
-                                                     T* __restrict__ dst, T fct, int ortho) {
+                                                     T* __restrict__ dst, T fct, int ortho,
+                                                     ImgLayout im = ImgLayout{0, 1, 1}) {
   __shared__ __attribute__((aligned(16))) T xs[32 * 72];
   const int tid = threadIdx.x, u = tid >> 3, r = tid & 7;
   for (int64_t g = blockIdx.x; g * 32 < nunit; g += gridDim.x) {
@@ -106,7 +114,19 @@ __global__ __launch_bounds__(256) void dct8x8_kernel(const TI* __restrict__ src,
     T x[8];
     if (unit < nunit) {
       alignas(16) TI v[8];
-      load8<TI>(src + unit * 64 + r * 8, v);
+      if constexpr (IMG) {
+        const int64_t by = unit / im.per_row, rem = unit - by * im.per_row;
+        const int64_t bx = rem / im.C, c = rem - bx * im.C;
+        const TI* p = src + ((8 * by + r) * im.W + 8 * bx) * im.C + c;
+        if (im.C == 1) {
+          load8<TI>(p, v);
+        } else {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) v[k] = p[k * im.C];
+        }
+      } else {
+        load8<TI>(src + unit * 64 + r * 8, v);
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) x[k] = (T)v[k];
     } else {
@@ -161,6 +181,39 @@ hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst
     else
       dct8x8_kernel<TI, double, false><<<grid, 256, 0, s>>>((const TI*)src, nblk, (double*)dst,
                                                             fct, ortho);
+  });
+  return hipGetLastError();
+}
+
+// DCT of the Patcher view of `rows` block rows of an [., W, C] image (dct.py:12-46 on
+// shape.py:45-54's view): dst [rows, W/8, C, 8, 8]
+hipError_t launch_dct8x8_image(const void* img, int src_dtype, int64_t rows, int64_t W, int64_t C,
+                               void* dst, int dst_dtype, int inverse, int norm, hipStream_t s) {
+  const int64_t nblk = rows * (W / 8) * C;
+  if (nblk <= 0) return hipSuccess;
+  const int inorm = inverse ? 2 - norm : norm;
+  const double fct = inorm == 0 ? 1.0 : (inorm == 1 ? 0.25 : 0.0625);
+  const int ortho = norm == IVC_NORM_ORTHO;
+  const unsigned grid = grid_for(nblk, 32, 8);
+  const ImgLayout im{W, C, W / 8 * C};
+  if (dst_dtype == IVC_F32) {
+    if (src_dtype != IVC_F32) return hipErrorInvalidValue;
+    if (inverse)
+      dct8x8_kernel<float, float, true, true><<<grid, 256, 0, s>>>((const float*)img, nblk,
+                                                                    (float*)dst, (float)fct, ortho, im);
+    else
+      dct8x8_kernel<float, float, false, true><<<grid, 256, 0, s>>>((const float*)img, nblk,
+                                                                     (float*)dst, (float)fct, ortho, im);
+    return hipGetLastError();
+  }
+  if (dst_dtype != IVC_F64 || src_dtype == IVC_F32) return hipErrorInvalidValue;
+  IVC_DISPATCH_ALL(src_dtype, {
+    if (inverse)
+      dct8x8_kernel<TI, double, true, true><<<grid, 256, 0, s>>>((const TI*)img, nblk,
+                                                                 (double*)dst, fct, ortho, im);
+    else
+      dct8x8_kernel<TI, double, false, true><<<grid, 256, 0, s>>>((const TI*)img, nblk,
+                                                                  (double*)dst, fct, ortho, im);
   });
   return hipGetLastError();
 }
@@ -724,6 +777,12 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
 // the wave's LDS region, ZR_WIN symbols at a time, and stores it with whole-wave
 // consecutive dword stores.
 constexpr int ZR_WIN = XS_PITCH * 8 * 8 / 4;   // int32 symbols in a wave's transpose region
+#ifndef IVC_EMIT_FIT
+#define IVC_EMIT_FIT 1                           // 0: every group through the general emission
+#endif
+#ifndef IVC_EMIT_MASK
+#define IVC_EMIT_MASK 1                          // fit path: run starts from scalar lane masks (0: DPP)
+#endif
 
 // Staging address of raster coefficient j inside a block-plane for the emission pass (the
 // count pass and OUT_COEFS stage in zig-zag order).  Zig-zag staging makes the quantiser's
@@ -831,9 +890,98 @@ __device__ __forceinline__ void zh_flush(const FusedArgs& a, const uint32_t* zh,
   }
 }
 
+// a lane's histogram bin for symbol v (branch-free: both bin forms, one select)
+__device__ __forceinline__ uint32_t zh_bin(const FusedArgs& a, int32_t v, int lane) {
+  const uint32_t h0 = (uint32_t)(v - ZH_HOT_LO);             // -8..7 -> 0..15
+  const uint32_t hv = v == a.zr_eob ? 16u : (h0 < 16u ? h0 : (uint32_t)ZH_HOT_N);
+  const uint32_t k = (uint32_t)(v + ZH_HALF);
+  const uint32_t hot = ZH_HOT + 32 * hv + (uint32_t)(lane & 31);
+  const uint32_t cold = k < (uint32_t)ZH_BINS ? k : (uint32_t)ZH_TRASH;
+  return hv < (uint32_t)ZH_HOT_N ? hot : cold;
+}
+
+// Emission of a whole group whose stream fits the wave's window (the count pass's count says
+// so, a.zr_counts): every block-plane's symbols are placed with VALU only — the run starts
+// come from the lane's own bits (zero, the previous lane nonzero by DPP, a nonzero later:
+// m >> lane != 0), their ballot feeds the lane's slot (two mbcnt) — so the scalar unit keeps
+// only the two popcounts and the running fill per block-plane, and no block has a window
+// check (one basic block for the group).  Same slots and values as the general path below.
+template <int C, bool DUP, bool HIST>
+__device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* os, int64_t gbase,
+                                                  int gcount, const int32_t (&xv)[8][(C == 1 && DUP) ? 2 : 3],
+                                                  ZrHistAcc& H) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;
+  constexpr int R1 = (C == 1 && DUP) ? 2 : 1;
+  const int lane = threadIdx.x & 63;
+  int32_t* zs = os;
+  int fill = 0;
+  const int32_t eob = a.zr_eob;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int32_t x = xv[b][p];
+      const bool nz = x != 0;
+      const uint64_t m = __ballot(nz);
+      const uint64_t later = m >> lane;                         // this lane's bit and above
+      const bool hl = later != 0;
+#if IVC_EMIT_MASK
+      // lane masks on the scalar unit: previous lane nonzero (lane 0: as if nonzero, a run may
+      // start there) and a nonzero at or after the lane
+      const uint64_t pm = (m << 1) | 1ull, hm = __ballot(hl);
+      const uint64_t st = pm & hm & ~m;                          // run starts before the last nonzero
+      const bool pnz = __builtin_amdgcn_inverse_ballot_w64(pm);
+      const bool rs = __builtin_amdgcn_inverse_ballot_w64(st);
+#else
+      // the previous lane's nz (lane 0: as if nonzero, a run may start there)
+      const bool pnz = __builtin_amdgcn_update_dpp(1, nz ? 1 : 0, 0x138, 0xf, 0xf, false) != 0;
+      const bool rs = !nz && pnz && hl;                         // a run start before the last nonzero
+      const uint64_t st = __ballot(rs);
+#endif
+      const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
+      const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
+                      2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
+      // a nonzero, a run's 0 + its length, or (the first zero after the last nonzero) the EOB
+      const bool w1 = nz || pnz;
+      const int32_t v1 = nz || hl ? x : eob;
+      const int32_t v2 = rs ? (int32_t)__builtin_ctzll(later) : eob;
+#pragma unroll
+      for (int k = 0; k < (p == 1 ? R1 : 1); ++k) {
+        int32_t* const d = w1 ? zs + fill + pos : zs + ZR_WIN - 65 + lane;
+        d[1] = v2;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // keep the two writes ordered
+        d[0] = v1;
+        fill += cnt;
+      }
+    }
+  }
+  (void)gcount;
+  __builtin_amdgcn_wave_barrier();
+  // the window -> the stream: a uniform loop; the store's buffer range drops slots past the
+  // group's stream (and past the caller's capacity), the histogram adds weight 0 there
+  const int64_t lim = a.zr_cap - gbase;
+  const int nst = (int)(lim < (int64_t)fill ? (lim > 0 ? lim : 0) : (int64_t)fill);
+  const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+      a.zr_out + (nst > 0 ? gbase : 0), 0, 4 * nst, 0x00020000);
+  for (int j0 = 0; j0 < fill; j0 += 64) {
+    const int j = j0 + lane;
+    const int32_t v = zs[j];
+    __builtin_amdgcn_raw_buffer_store_b32(v, ro, 4 * j, 0, 0);
+    if constexpr (HIST) {
+      const bool in = j < fill;
+      const uint32_t kb = zh_bin(a, v, lane);
+      atomicAdd(H.bins + kb, in ? 1u : 0u);
+      if (__builtin_expect(__ballot(in && kb == (uint32_t)ZH_TRASH) != 0, 0)) {
+        if (in && kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v, 1u);
+      }
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int C, bool DUP, bool HIST>
 __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, int nb,
-                                              int64_t gbase, ZrHistAcc& H) {
+                                              int64_t gbase, int gcount, ZrHistAcc& H) {
   constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging
   constexpr int PITCH = os_pitch<C, DUP>();
   const int lane = threadIdx.x & 63;
@@ -844,6 +992,10 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
 #pragma unroll
     for (int p = 0; p < NP; ++p) xv[b][p] = os[b * PITCH + p * 64 + ra];
   __builtin_amdgcn_wave_barrier();              // staging read: the region becomes the window
+  if (IVC_EMIT_FIT && nb == 8 && gcount <= ZR_WIN - 65) {
+    zr_group_emit_fit<C, DUP, HIST>(a, os, gbase, gcount, xv, H);
+    return;
+  }
   int32_t* zs = os;
   int64_t base = gbase;
   int fill = 0;
@@ -924,7 +1076,7 @@ template <int C, bool DUP, int OUTM>
 __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b, int r, int nb,
                                          int64_t gid, ZrHistAcc& H) {
   if constexpr (OUTM == OUT_SYMBOLS || OUTM == OUT_SYMH) {
-    zr_group_emit<C, DUP, OUTM == OUT_SYMH>(a, os, nb, a.zr_off[gid], H);
+    zr_group_emit<C, DUP, OUTM == OUT_SYMH>(a, os, nb, a.zr_off[gid], a.zr_counts[gid], H);
     return;
   }
   constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging

@@ -67,6 +67,13 @@ __host__ __device__ constexpr int wave_dy0(int w) { return 8 * w; }
 __host__ __device__ constexpr int wave_ndy(int w) { return w == 3 ? 9 : 8; }
 }  // namespace mf
 
+#ifndef IVC_ME_SWP
+#define IVC_ME_SWP 1         // software-pipelined M-tiles (0: operands read at each M-tile)
+#endif
+#ifndef IVC_ME_SWP_R
+#define IVC_ME_SWP_R 4       // rows (and E words) of the next M-tile read ahead
+#endif
+
 typedef int mf_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned int mf_u32x2 __attribute__((ext_vector_type(2)));
 
@@ -253,7 +260,86 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
                     __builtin_amdgcn_mov_dpp(x.w, c, 0xf, 0xf, false)};
     };
     mf_v4i bk = rot(bop, std::integral_constant<int, 0x93>{});   // r = 3: quads 3, 0, 1, 2
+    mf_v4i bks = mf_v4i{bk.z, bk.w, bk.x, bk.y};      // block rows 2g + 1 | 2g
     int acc0 = INT_MIN, acc1 = INT_MIN;                 // running best key of quads k - 1, k
+#if IVC_ME_SWP
+    // software-pipelined M-tiles: M-tile mt + 1's operands (10 reference rows and 9 E words
+    // per lane) are read from LDS while M-tile mt's MFMAs run, so the steps never wait on LDS
+    // latency.  Every wave runs a ninth step (dy = dyw0 + 8) so that an M-tile is one basic
+    // block; in waves 0-2 (8 dy each) its C operand masks every output (below VALID_MIN).
+    // (the first SWP_R rows and E words of an M-tile are prefetched; the rest are read at the
+    // M-tile's start, ahead of the steps that need them)
+    constexpr int PR = IVC_ME_SWP_R < 10 ? IVC_ME_SWP_R : 10, PE = PR < 9 ? PR : 9;
+    struct MtOps {
+      mf_u32x2 r[PR];                                   // rows dyw0 + 2g + kk, bytes u .. u+7
+      int e[PE];                                        // E[dyw0 + d][u]
+    };
+    auto row_at = [&](int mt, int kk) {
+      const int wd = 4 * mt + (l16 >> 2);               // word of window position u = 16 mt + l16
+      const int rr = dyw0 + 2 * g + kk;
+      return mf_u32x2{cb[rr * PITCH + wd], cb[rr * PITCH + wd + 1]};
+    };
+    auto load_mt = [&](int mt, MtOps& L) {
+#pragma unroll
+      for (int kk = 0; kk < PR; ++kk) L.r[kk] = row_at(mt, kk);
+#pragma unroll
+      for (int d = 0; d < PE; ++d) L.e[d] = ev[16 * mt + d * U];
+    };
+    // the window operand of step dl is rows (dl, dl + 1): one 4-dword tuple T = [P | Q] serves
+    // every step without register copies (step dl + 1 overwrites the half holding row dl with
+    // row dl + 2, and odd steps use the block operand with its halves swapped)
+    auto do_mt = [&](int mt, const MtOps& L, int q0, int q1, const mf_v4i& bk, const mf_v4i& bks) {
+      mf_u32x2 rt[10 - PR > 0 ? 10 - PR : 1];
+      int et[9 - PE > 0 ? 9 - PE : 1];
+#pragma unroll
+      for (int kk = PR; kk < 10; ++kk) rt[kk - PR] = row_at(mt, kk);
+#pragma unroll
+      for (int d = PE; d < 9; ++d) et[d - PE] = ev[16 * mt + d * U];
+      auto rowv = [&](int kk) { return kk < PR ? L.r[kk < PR ? kk : 0] : rt[kk >= PR ? kk - PR : 0]; };
+      auto ev_ = [&](int d) { return d < PE ? L.e[d < PE ? d : 0] : et[d >= PE ? d - PE : 0]; };
+      const int v0 = 16 * mt + cj - 32 * q0, v1 = 16 * mt + cj - 32 * q1;
+      const mf_v4i cm = mf_v4i{(unsigned)v0 <= 32u ? 0 : MASK_C, (unsigned)v1 <= 32u ? 0 : MASK_C, 0, 0};
+      const mf_v4i cm8 = wave == 3 ? cm : mf_v4i{MASK_C, MASK_C, 0, 0};
+      mf_v4i T;
+      {
+        const mf_u32x2 r0 = rowv(0), r1 = rowv(1);
+        T = mf_v4i{(int)r0.x, (int)r0.y, (int)r1.x, (int)r1.y};
+      }
+#pragma unroll
+      for (int dl = 0; dl < 9; ++dl) {
+        if (dl > 0) {
+          const mf_u32x2 rn = rowv(dl + 1);
+          if (dl & 1) {
+            T.x = (int)rn.x;
+            T.y = (int)rn.y;
+          } else {
+            T.z = (int)rn.x;
+            T.w = (int)rn.y;
+          }
+        }
+        const mf_v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8((dl & 1) ? bks : bk, T,
+                                                               dl == 8 ? cm8 : cm, 0, 0, 0);
+        const uint32_t e = (uint32_t)ev_(dl);
+        acc0 = max(acc0, (int)(((uint32_t)d.x << 8) + e));
+        acc1 = max(acc1, (int)(((uint32_t)d.y << 8) + e));
+      }
+    };
+    MtOps LA, LB;
+    load_mt(0, LA);
+#pragma unroll 1
+    for (int k = 0; k < NMT / 2; ++k) {
+      const int q0 = (k + 3) & 3, q1 = k & 3;
+      load_mt(2 * k + 1, LB);
+      do_mt(2 * k, LA, q0, q1, bk, bks);
+      load_mt(2 * k + 2 < NMT ? 2 * k + 2 : NMT - 1, LA);
+      do_mt(2 * k + 1, LB, q0, q1, bk, bks);
+      if (k > 0) finish(q0, acc0);                      // quad k - 1 is complete
+      acc0 = acc1;
+      acc1 = INT_MIN;
+      bk = rot(bk, std::integral_constant<int, 0x39>{});  // r + 1: quad_perm 1,2,3,0
+      bks = mf_v4i{bk.z, bk.w, bk.x, bk.y};
+    }
+#else
 #pragma unroll 1
     for (int k = 0; k < NMT / 2; ++k) {
       const int q0 = (k + 3) & 3, q1 = k & 3;
@@ -266,16 +352,32 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
         const int* em = ev + 16 * mt;                   // E[dyw0 ..][u]
         const mf_v4i e0 = mf_v4i{em[0], em[U], em[2 * U], em[3 * U]};
         const mf_v4i e1 = mf_v4i{em[4 * U], em[5 * U], em[6 * U], em[7 * U]};
-        mf_u32x2 r[10];                                 // rows dyw0 + 2g + k, bytes u .. u+7
-#pragma unroll
-        for (int kk = 0; kk < 10; ++kk) {
-          const int row = dyw0 + 2 * g + kk;
-          r[kk] = (kk < 9 || wave == 3) ? mf_u32x2{cb[row * PITCH + wd], cb[row * PITCH + wd + 1]}
-                                        : mf_u32x2{0u, 0u};
+        // the window operand of step dl is rows (dl, dl + 1) (+ dyw0 + 2g), bytes u .. u+7.  One
+        // 4-dword tuple T = [P | Q] serves every step without register copies: step dl + 1
+        // overwrites the half holding row dl with row dl + 2, so the tuple alternates between
+        // [row dl | row dl + 1] (even dl, block operand bk: block rows 2g | 2g + 1) and
+        // [row dl + 1 | row dl] (odd dl, bks: the block operand with its halves swapped)
+        auto row = [&](int kk) {
+          const int rr = dyw0 + 2 * g + kk;
+          return mf_u32x2{cb[rr * PITCH + wd], cb[rr * PITCH + wd + 1]};
+        };
+        mf_v4i T;
+        {
+          const mf_u32x2 r0 = row(0), r1 = row(1);
+          T = mf_v4i{(int)r0.x, (int)r0.y, (int)r1.x, (int)r1.y};
         }
         auto step = [&](int dl, uint32_t e) {
-          const mf_v4i aop = mf_v4i{(int)r[dl].x, (int)r[dl].y, (int)r[dl + 1].x, (int)r[dl + 1].y};
-          const mf_v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8(bk, aop, cm, 0, 0, 0);
+          if (dl > 0) {
+            const mf_u32x2 rn = row(dl + 1);
+            if (dl & 1) {
+              T.x = (int)rn.x;
+              T.y = (int)rn.y;
+            } else {
+              T.z = (int)rn.x;
+              T.w = (int)rn.y;
+            }
+          }
+          const mf_v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8((dl & 1) ? bks : bk, T, cm, 0, 0, 0);
           acc0 = max(acc0, (int)(((uint32_t)d.x << 8) + e));
           acc1 = max(acc1, (int)(((uint32_t)d.y << 8) + e));
         };
@@ -293,7 +395,9 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
       acc0 = acc1;
       acc1 = INT_MIN;
       bk = rot(bk, std::integral_constant<int, 0x39>{});  // r + 1: quad_perm 1,2,3,0
+      bks = mf_v4i{bk.z, bk.w, bk.x, bk.y};
     }
+#endif
     __syncthreads();
     if (tid < TB) {
       const int j = tid, bx = bx0 + j;

@@ -11,6 +11,20 @@ import numpy as np
 from .. import _native as N
 
 
+def patch_view_image(x):
+    """If x is Patcher.patch's view of a C-contiguous [H, W, C] image (shape.py:45-54:
+    [H/8, W/8, C, 8, 8] with strides (8 W C, 8 C, 1, W C, C) elements), that image as an
+    [H, W, C] array over the same memory; else None."""
+    if x.ndim != 5 or x.shape[-2:] != (8, 8) or x.flags.c_contiguous:
+        return None
+    h, w, C = x.shape[:3]
+    s = x.itemsize
+    W = 8 * w
+    if x.strides != (8 * W * C * s, 8 * C * s, s, W * C * s, C * s):
+        return None
+    return np.lib.stride_tricks.as_strided(x, shape=(8 * h, W, C), strides=(W * C * s, C * s, s))
+
+
 def dct2d(a, norm="ortho", inverse=False) -> np.ndarray:
     """dct (or idct) along axis -1 then axis -2 of every trailing 8x8 block of `a`."""
     if norm not in N.NORM_CODE:
@@ -37,8 +51,14 @@ def dct2d(a, norm="ortho", inverse=False) -> np.ndarray:
     nblk = x.size // 64
     if nblk == 0:
         return out
-    x = np.ascontiguousarray(x)
     L = N.lib()
+    img = patch_view_image(x)
+    if img is not None:          # transform(patch(img)): the kernel reads the image in place
+        N.check(L.ivc_dct8x8_image(N.ptr(img), N.DTYPE_CODE[img.dtype], img.shape[0], img.shape[1],
+                                   img.shape[2], N.ptr(out), N.DTYPE_CODE[np.dtype(out_dtype)],
+                                   1 if inverse else 0, N.NORM_CODE[norm]), "DiscreteCosineTransform")
+        return out
+    x = np.ascontiguousarray(x)
     N.check(L.ivc_dct8x8(N.ptr(x), N.DTYPE_CODE[x.dtype], nblk, N.ptr(out),
                          N.DTYPE_CODE[np.dtype(out_dtype)], 1 if inverse else 0,
                          N.NORM_CODE[norm]), "DiscreteCosineTransform")

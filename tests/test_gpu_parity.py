@@ -44,6 +44,75 @@ def rand_array(rng, dtype, shape):
 
 
 # ------------------------------------------------------------------------ DCT ----------
+@pytest.mark.parametrize("C", [1, 3, 2])
+@pytest.mark.parametrize("dtype", [np.uint8, np.float64, np.float32, np.int16])
+def test_dct_of_patch_view_read_in_place(C, dtype):
+    """DCT.transform(Patcher.patch(img)) reads the image in place (ivc_dct8x8_image: the
+    kernel addresses the view, dct.py:12-28 on shape.py:45-54); the result equals the
+    transform of the gathered view and the oracle's, for both directions, on a frame large
+    enough for the chunked host pipeline and on one that is not."""
+    rng = np.random.default_rng(7 + C)
+    from ivclab_amd.signal.dct import patch_view_image
+    for H, W in ((48, 72), (1080, 1920)):
+        img = rand_array(rng, dtype, (H, W, C))
+        p = Patcher().patch(img)
+        assert patch_view_image(p) is not None
+        for inv in (False, True):
+            f = DCT.inverse_transform if inv else DCT.transform
+            o = O.dct_inverse if inv else O.dct_transform
+            got = f(p)
+            assert_bits(got, f(np.ascontiguousarray(p)), f"view vs gathered C={C} {dtype} inv={inv}")
+            if H == 48:
+                assert_bits(got, o(p), f"view vs oracle C={C} {dtype} inv={inv}")
+    # a view of a non-contiguous image is gathered as before
+    img = rand_array(rng, dtype, (48, 72, C))[:, ::-1]
+    p = Patcher().patch(img)
+    assert patch_view_image(p) is None
+    assert_bits(DCT.transform(p), O.dct_transform(p), "reversed view")
+
+
+def test_host_pipeline_chunking_changes_nothing():
+    """Host-buffer calls with page-locked results go in chunks on 3 streams
+    (ivc_set_host_pipeline); every chunk size, and none, gives the same bits."""
+    from ivclab_amd import _native as N
+    rng = np.random.default_rng(3)
+    img = rng.integers(0, 256, (2160, 3840, 1), dtype=np.uint8)
+    pq, zz, pt = PatchQuant(0.7), ZigZag(), Patcher()
+    L = N.lib()
+    outs = []
+    try:
+        for chunk in (0, 1 << 20, 3 << 20, 8 << 20):
+            N.check(L.ivc_set_host_pipeline(chunk))
+            d = DCT.transform(pt.patch(img))
+            q = pq.quantize(d)
+            z = zz.flatten(q)
+            outs.append((d, q, z, pq.dequantize(q), zz.unflatten(z)))
+    finally:
+        N.check(L.ivc_set_host_pipeline(8 << 20))
+    for o in outs[1:]:
+        for a, b in zip(o, outs[0]):
+            assert_bits(a, b, "pipelined vs one piece")
+    assert_bits(outs[0][2].reshape(-1, 64), O.zigzag_flatten(O.quantize(O.dct_transform(pt.patch(img)), 0.7)).reshape(-1, 64), "vs oracle")
+
+
+def test_tiny_calls_zero_copy():
+    """One (8, 8) block, a (3, 8, 8) stack, one zig-zag row: the tiny-call path (the kernel
+    reads and writes a mapped page-locked block) against the oracle, many calls in a row."""
+    rng = np.random.default_rng(5)
+    pq = PatchQuant(0.5)
+    zz = ZigZag()
+    for _ in range(50):
+        blk = rng.normal(0, 90, (8, 8))
+        assert_bits(DCT.transform(blk), O.dct_transform(blk), "8x8")
+        assert_bits(DCT.inverse_transform(blk), O.dct_inverse(blk), "8x8 inverse")
+        stk = rng.normal(0, 40, (3, 8, 8))
+        assert_bits(pq.quantize(stk), O.quantize(stk, 0.5), "3x8x8")
+        q = pq.quantize(stk)
+        assert_bits(pq.dequantize(q), O.dequantize(q, 0.5), "dequantize")
+        z = zigzag_scan(blk.astype(np.int32))
+        assert_bits(z, O.zigzag_scan(blk.astype(np.int32)), "zigzag_scan")
+
+
 def test_dct_golden(golden):
     d = golden("dct")
     assert_bits(DCT.transform(d["x_u8"]), d["dct_u8"], "dct u8")

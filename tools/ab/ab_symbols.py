@@ -20,6 +20,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("libs", nargs="+")
 ap.add_argument("--frames", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--legs", default="", help="comma-separated subset of the legs")
 args = ap.parse_args()
 N.load_library()
 libs = []
@@ -49,7 +50,7 @@ nsd = torch.zeros(1, dtype=torch.int64, device=dev)
 hist = torch.zeros(4200, dtype=torch.int64, device=dev)
 mm = torch.empty(2, dtype=torch.int32, device=dev)
 hist2 = torch.zeros(8194, dtype=torch.int64, device=dev)
-img = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
+rgb = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
 err = torch.zeros(3, dtype=torch.int64, device=dev)
 
 
@@ -74,13 +75,29 @@ legs = {
         img.data_ptr(), 1, F, H, W, 1, t.ctypes.data, 4000, sym.data_ptr(), nsym, nsd.data_ptr(),
         hist2.data_ptr(), -4097, 8194, stream))),
     "symbols2image": lambda L: N.check(L.ivc_symbols2image_dev(
-        sym.data_ptr(), nsym, F, H, W, 3, t.ctypes.data, 4000, 1, img.data_ptr(), err.data_ptr(),
+        sym.data_ptr(), nsym, F, H, W, 3, t.ctypes.data, 4000, 1, rgb.data_ptr(), err.data_ptr(),
         stream)),
     "histogram": lambda L: (hist.zero_(), N.check(L.ivc_histogram_i32_dev(
         sym.data_ptr(), nsym, -64, 4200, hist.data_ptr(), stream))),
     "minmax": lambda L: N.check(L.ivc_minmax_i32_dev(sym.data_ptr(), nsym, mm.data_ptr(), stream)),
 }
+if args.legs:
+    legs = {k: v for k, v in legs.items() if k in args.legs.split(",")}
 res = {(leg, n): [] for leg in legs for n, _ in libs}
+
+
+def digest_of(x):
+    """Whole-tensor checksum (chunked: int64 sum and an index-weighted sum of the words)."""
+    v = x.view(-1)
+    v = v.view(torch.int64) if v.dtype == torch.float64 else v
+    s1 = s2 = 0
+    CH = 1 << 26
+    for i in range(0, v.numel(), CH):
+        c = v[i:i + CH].to(torch.int64)
+        w = (torch.arange(i, i + c.numel(), device=c.device, dtype=torch.int64) % 7919) + 1
+        s1 += int(c.sum().item())
+        s2 += int((c * w).sum().item())
+    return (s1, s2, int(v.numel()))
 check = {}
 for rnd in range(args.rounds):
     for leg, fn in legs.items():
@@ -89,11 +106,8 @@ for rnd in range(args.rounds):
             if rnd == 0:
                 torch.cuda.synchronize()
                 outs = {"zerorun_encode": sym, "intra_symbols": sym, "symbols_hist": hist2,
-                        "symbols2image": img, "histogram": hist, "minmax": mm}
-                o = outs[leg].view(-1)[:1 << 24]
-                o = o.view(torch.int64) if o.dtype == torch.float64 else o.to(torch.int64)
-                digest = (int(o.sum().item()),
-                          int(outs[leg].numel()))
+                        "symbols2image": rgb, "histogram": hist, "minmax": mm}
+                digest = digest_of(outs[leg])
                 check.setdefault(leg, digest)
                 if digest != check[leg]:
                     print(f"MISMATCH {leg} {n}: {digest} vs {check[leg]}", flush=True)

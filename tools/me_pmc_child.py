@@ -1,6 +1,6 @@
-"""Profiling child: the cfg4 motion search alone (1080p x 300 u8, +-16, exact SSD: the S2
-pre-pass and me_fast_u8_kernel<16>), twice, then the float64 NumPy-semantics search on 60
-frames once.  Run under `rocprofv3 --pmc ...` (tools/gpu_r02d.sh); prints nothing timed."""
+"""Profiling child: the cfg4 motion search alone (1080p x 300 u8, +-16, exact SSD: the
+matrix-core me_mfma16_kernel), twice, then (unless ME_NO_F64=1) the float64 NumPy-semantics
+search on 60 frames once.  Run under `rocprofv3 --pmc ...` (tools/gpu_pmc_child.sh); prints nothing timed."""
 import os
 import sys
 
@@ -21,9 +21,10 @@ def main():
     mv = torch.empty((F - 1, 135, 240), dtype=torch.int64, device=dev)
     for _ in range(2):
         D.motion_estimate(seq[:-1], seq[1:], 16, mv, exact_u8=True)
-    y = bench.luma_f64(seq[:60]).contiguous()
-    mvf = torch.empty((59, 135, 240), dtype=torch.int64, device=dev)
-    D.motion_estimate(y[:-1], y[1:], 16, mvf)
+    if os.environ.get("ME_NO_F64") != "1":
+        y = bench.luma_f64(seq[:60]).contiguous()
+        mvf = torch.empty((59, 135, 240), dtype=torch.int64, device=dev)
+        D.motion_estimate(y[:-1], y[1:], 16, mvf)
     torch.cuda.synchronize()
     print("me_pmc_child done")
 
