@@ -545,7 +545,7 @@ def leg_luma_only(args, dist, rank, world, dev, table, frames, result, verify):
     wall, ms = timed(dist, step, args.steps, args.warmup, sync_warmup=True)
     algo = F * H * W * 5
     result["luma_only"] = {
-        "metric": "Mpixels/s: 4K intra DCT+quant, luma-table plane only (not the reference's 3-plane output)",
+        "metric": "Mpixels/s: 4K intra DCT+quant, luma-table plane only (not the reference's 3-plane output), unpaced",
         "value": round(world * F * H * W * args.steps / wall / 1e6, 1), "unit": "Mpixels/s",
         "ms_per_step": round(wall / args.steps * 1e3, 3),
         "roofline": {"bound": "hbm", "kernel": "fused_encode_kernel<u8,f64,C=1,OUT_LUMA>",
@@ -766,8 +766,8 @@ def leg_inter(args, dist, rank, world, dev, table, result, verify):
         "ms_per_step": round(iwall / args.inter_steps * 1e3, 3),
         "config": {"workload": f"cfg4: {Fi} frames 1920x1080 u8 luma per GPU, sr={sr}, "
                                "ME against the previous source frame (open loop)"},
-        "roofline": {"bound": "valu (per-output key selection)" if mfma else "valu (v_dot4_u32_u8)",
-                     "kernel": "me_mfma16_kernel" if mfma else "me_s2_kernel<true> + me_tile16_kernel",
+        "roofline": {"bound": "latency (LDS / barriers; issue ~40%)" if mfma else "valu (v_dot4_u32_u8)",
+                     "kernel": "me_mfma16x2_kernel" if mfma else "me_s2_kernel<true> + me_tile16_kernel",
                      "kernel_ms": round(me_ms, 4),
                      "achieved": round(dot4 / (me_ms * 1e-3) / 1e12, 2), "peak": round(DOT4_PEAK_T, 2),
                      "unit": "T dot4 lane-ops/s", "frac": round(dot4 / (me_ms * 1e-3) / 1e12 / DOT4_PEAK_T, 4),
@@ -778,9 +778,10 @@ def leg_inter(args, dist, rank, world, dev, table, result, verify):
                      "note": ("useful work = valid candidates x 64 px (SSD = sum c^2 + S2 - 2X); frac is "
                               "the dot4-equivalent rate (candidates x 16 dot4 lane-ops against the "
                               "half-rate dot4 VALU peak) so both search kernels share one scale; "
-                              + ("the matrix-core kernel computes 16 blocks x 16 window positions per "
-                                 "MFMA (20.6% of its outputs are candidates) and is bound by the VALU "
-                                 "selection of those outputs, not by the MFMA pipe (mfma_i8.frac)"
+                              + ("the matrix-core kernel computes 16 blocks (8 of two block rows) x 16 "
+                                 "window positions per MFMA and turns only the live result registers "
+                                 "into keys (DESIGN.md §5); it is neither MFMA- nor VALU-issue-bound "
+                                 "(mfma_i8.frac; PMC in profiles/)"
                                  if mfma else "S2 pre-pass time included"))},
     }
     if verify is not None:
@@ -838,6 +839,44 @@ def leg_inter_f64(args, dist, rank, world, dev, seq_u8, result, verify):
         verify["checked"].append(f"inter_f64: pair {p} whole vs C oracle (NumPy pairwise SSD)")
 
 
+def leg_cfg2(args, dist, rank, world, dev, table, result, verify):
+    """BASELINE configs[1] device-resident: 1920x1080 RGB u8, per-channel DCT + quantise +
+    zig-zag (patchquant.py:44-60, shape.py:21-28) in the fused kernel (C = 3), one frame per
+    launch (launch-bound at this size) and a 64-frame batch per launch; HBM roofline at
+    15 B/px (3 B in + 3 planes x 4 B out)."""
+    import ivclab_amd.device as D
+    F, H, W = args.cfg2_frames, 1080, 1920
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    frames = torch.randint(0, 256, (F, H, W, 3), device=dev, generator=g, dtype=torch.uint8)
+    out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+    res = {}
+    for label, nf, reps in (("one_frame", 1, 200), (f"batch_{F}", F, 20)):
+        fr, o = frames[:nf], out[:nf]
+        wall, ms = timed(dist, lambda: D.intra_encode(fr, table, o, zigzag=True), reps, 5)
+        algo = nf * H * W * 15
+        res[label] = {"frames": nf, "ms_per_launch": round(ms, 4),
+                      "Mpixels_per_s": round(world * nf * H * W * reps / wall / 1e6, 1),
+                      "roofline": {"bound": "hbm", "kernel": "fused_encode_kernel<u8,f64,C=3,ZZ>",
+                                   "kernel_ms": round(ms, 4),
+                                   "achieved": round(algo / (ms * 1e-3) / 1e9, 1),
+                                   "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                   "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "algorithmic_bytes_per_launch": algo}}
+    if verify is not None:
+        from oracle import ivc_oracle as O
+        torch.cuda.synchronize()
+        for f in sorted({0, F - 1}):
+            want = O.intra_encode(frames[f].cpu().numpy(), 1.0, zigzag=True)
+            check_equal(out[f].cpu().numpy(), want.reshape(out[f].shape), f"cfg2 frame {f}",
+                        verify["failures"])
+        verify["checked"].append(f"cfg2: frames [0, {F - 1}] of the batch whole vs oracle")
+    result["cfg2"] = dict(res, workload="cfg2: 1920x1080 RGB u8, per-channel DCT + quant + "
+                                        "zig-zag, device-resident (15 B/px)")
+    del frames, out
+    torch.cuda.empty_cache()
+
+
 def leg_class_api(args, dev, result, verify):
     """Host arrays through the drop-in classes (each call stages H2D, runs its kernel and
     copies back, as a NumPy caller sees it) and through the one-call host entry point."""
@@ -881,7 +920,30 @@ def leg_class_api(args, dev, result, verify):
                             verify["failures"])
         res["shape"] = list(img.shape)
         out[name] = res
+    # the reference's per-block loop calls (exercises/ch3/E3-1_claude.py:47-60): one (8, 8)
+    # block through transform, one (3, 8, 8) stack through quantize, per call, beside the same
+    # call of the oracle (scipy / NumPy) on this host
+    from oracle import ivc_oracle as O
+    blk = rng.integers(0, 256, (8, 8)).astype(np.float64)
+    stk = rng.normal(0, 50, (3, 8, 8))
+
+    def per_call_us(fn, reps=300):
+        fn()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        return round((time.perf_counter() - t0) / reps * 1e6, 2)
+
+    out["small_call"] = {
+        "transform_8x8_us": per_call_us(lambda: dct.transform(blk)),
+        "transform_8x8_numpy_us": per_call_us(lambda: O.dct_transform(blk)),
+        "quantize_3x8x8_us": per_call_us(lambda: pq.quantize(stk)),
+        "quantize_3x8x8_numpy_us": per_call_us(lambda: O.quantize(stk, 1.0)),
+        "note": "one launch + one sync per call (zero-copy: the kernel reads and writes a mapped "
+                "page-locked block); NumPy is faster per call at this size"}
     if verify is not None:
+        check_equal(dct.transform(blk), O.dct_transform(blk), "small_call transform", verify["failures"])
+        check_equal(pq.quantize(stk), O.quantize(stk, 1.0), "small_call quantize", verify["failures"])
         verify["checked"].append("class_api: every timed output vs oracle")
     result["class_api"] = dict(out, note="host NumPy in -> host NumPy out, PCIe included "
                                          "(DCT.transform -> PatchQuant.quantize -> ZigZag.flatten "
@@ -1024,6 +1086,8 @@ def parse(argv=None):
     ap.add_argument("--no-decode", action="store_true", help="skip the symbols2image leg")
     ap.add_argument("--no-luma", action="store_true", help="skip the luma-only (5 B/px) leg")
     ap.add_argument("--no-class-api", action="store_true", help="skip the host-buffer leg")
+    ap.add_argument("--no-cfg2", action="store_true", help="skip the device-resident cfg2 leg")
+    ap.add_argument("--cfg2-frames", type=int, default=64)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--rccl", action="store_true",
                     help="at 1 rank, run the histogram exchange through a one-rank RCCL group")
@@ -1100,6 +1164,8 @@ def main():
     # ---- host buffers through the classes (PCIe included) ---------------------------------
     if rank == 0 and not args.no_class_api:
         leg_class_api(args, dev, result, verify)
+    if not args.no_cfg2:
+        leg_cfg2(args, dist, rank, world, dev, table, result, verify)
 
     # ---- cfg5: 8K x 120 frames, frame-sharded ME + DCT, one all-gather of histograms ------
     if not args.no_sharded:

@@ -60,16 +60,18 @@ int ivc_set_device(int device);
 /* 1 if the loaded code object matches the current device (gfx950), 0 otherwise */
 int ivc_device_ok(void);
 /* Host-buffer calls whose output is in page-locked memory (ivc_host_alloc) move their data in
- * chunks of chunk_bytes (the larger of input and output per chunk; default 8 MiB) that go
+ * chunks of chunk_bytes (the larger of input and output per chunk) that go
  * upload -> kernel -> download on 3 streams, overlapping one chunk's copies with another's;
- * 0 runs every call in one piece.  Process-wide.                                          */
+ * 0 (the default: a half-duplex host link gains nothing from it) runs every call in one
+ * piece.  Process-wide.                                                                   */
 int ivc_set_host_pipeline(int64_t chunk_bytes);
 /* release the library's cached scratch buffers on the current device, and the pinned host
  * blocks ivc_host_free has cached (process-wide)                                          */
 int ivc_release_scratch(void);
 /* Page-locked host memory for the host-buffer entry points' arrays: a transfer from or to a
  * block of ivc_host_alloc is one DMA (no staging copy); freed blocks are cached by size and
- * reused, up to 1 GiB (env IVC_HOST_CACHE_MB overrides; ivc_release_scratch drains it).  NULL when the runtime cannot pin more memory.                                   */
+ * reused, up to 1 GiB (the oldest go first; env IVC_HOST_CACHE_MB overrides;
+ * ivc_release_scratch drains it).  NULL when the runtime cannot pin more memory.          */
 void* ivc_host_alloc(int64_t bytes);
 int ivc_host_free(void* p);
 /* Store pacing of the fused coefficient encoders (ivc_intra_encode*, ivc_inter_encode*):

@@ -8,6 +8,7 @@
 
 #include <condition_variable>
 #include <functional>
+#include <list>
 #include <map>
 #include <atomic>
 #include <mutex>
@@ -103,11 +104,12 @@ class CopyPool {
 // ivc_host_alloc: page-locked host memory the drop-in classes allocate their NumPy results in
 // (ivclab_amd._native.empty).  A transfer between such a block and the device is one DMA at
 // full PCIe speed with no CPU copy and no first-touch page faults; freed blocks are cached by
-// size (up to host_cache_max(): 1 GiB, or IVC_HOST_CACHE_MB) so repeated calls of the same
-// shapes reuse them; ivc_release_scratch returns the cached blocks to the system.
+// size (up to host_cache_max(): 1 GiB, or IVC_HOST_CACHE_MB; past it the oldest cached blocks
+// are released) so repeated calls of the same shapes reuse them; ivc_release_scratch returns
+// the cached blocks to the system.
 std::mutex g_host_mu;
 std::map<uintptr_t, size_t> g_host_live;          // block start -> bytes
-std::multimap<size_t, void*> g_host_cache;        // freed blocks by size
+std::list<std::pair<size_t, void*>> g_host_cache; // freed blocks, oldest first
 size_t g_host_cached = 0;
 constexpr size_t kHostGrain = 2u << 20;
 
@@ -148,8 +150,11 @@ constexpr size_t kPinChunk = 8u << 20;      // bytes per pinned slot
 constexpr size_t kPinMin = 1u << 20;        // smaller transfers go straight from pageable memory
 constexpr int kAux = 3;                     // pipelined host-buffer calls: streams
 constexpr size_t kPipeMin = 4u << 20;       // smaller outputs go in one piece
-// bytes per pipelined chunk (the larger of in / out); 0 = no pipelining (ivc_set_host_pipeline)
-std::atomic<size_t> g_pipe_chunk{8u << 20};
+// bytes per pipelined chunk (the larger of in / out); 0 = no pipelining (ivc_set_host_pipeline).
+// Off by default: on the MI355X boxes measured the host link is effectively half duplex
+// (56.6 GB/s one way, 27.5 GB/s each way at once), so overlapping one chunk's upload with
+// another's download gains nothing and the chunking costs 5-12 % (profiles/r04g_class_api.json)
+std::atomic<size_t> g_pipe_chunk{0};
 struct DevCtx {
   std::mutex mu;
   hipStream_t stream = nullptr;
@@ -474,7 +479,10 @@ void* ivc_host_alloc(int64_t bytes) {
   const size_t n = ((size_t)bytes + kHostGrain - 1) / kHostGrain * kHostGrain;
   std::lock_guard<std::mutex> g(g_host_mu);
   void* p = nullptr;
-  auto it = g_host_cache.find(n);
+  // the most recently freed block of this size
+  auto it = g_host_cache.end();
+  for (auto j = g_host_cache.begin(); j != g_host_cache.end(); ++j)
+    if (j->first == n) it = j;
   if (it != g_host_cache.end()) {
     p = it->second;
     g_host_cache.erase(it);
@@ -494,12 +502,18 @@ int ivc_host_free(void* p) {
   if (it == g_host_live.end()) return fail(IVC_E_ARG, "ivc_host_free: not a block of ivc_host_alloc");
   const size_t n = it->second;
   g_host_live.erase(it);
-  if (g_host_cached + n <= host_cache_max()) {
-    g_host_cache.emplace(n, p);
-    g_host_cached += n;
-  } else {
+  if (n > host_cache_max()) {
     (void)hipHostFree(p);
+    return IVC_OK;
   }
+  // keep the newest: the oldest cached blocks go back to the system to make room
+  while (g_host_cached + n > host_cache_max() && !g_host_cache.empty()) {
+    (void)hipHostFree(g_host_cache.front().second);
+    g_host_cached -= g_host_cache.front().first;
+    g_host_cache.pop_front();
+  }
+  g_host_cache.emplace_back(n, p);
+  g_host_cached += n;
   return IVC_OK;
 }
 

@@ -289,14 +289,8 @@ constexpr int SYM_QP = 72;                             // int16 per staged block
 constexpr int SYM_XW = SYM_SEG + 8;                    // int32 words: [3] = prev, [4 ..] symbols
 constexpr int SYM_XD = (SYM_XW / 2 > DX_WAVE ? SYM_XW / 2 : DX_WAVE);   // doubles per wave
 
-#ifndef IVC_S2I_PF
-#define IVC_S2I_PF 5            // 16-byte loads per lane of the next group's first round in flight
-#endif
-#ifndef IVC_S2I_WPE
-#define IVC_S2I_WPE 3           // waves per SIMD the kernel is compiled for (registers)
-#endif
 template <int C, bool RGB, bool FASTDQ>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IVC_S2I_WPE))) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t) {
   constexpr int QS = 8 * C * SYM_QP;                   // int16 per wave
   __shared__ __attribute__((aligned(16))) int16_t qs_all[4 * QS];
   __shared__ int bps_all[4 * 32];                       // block-plane start offsets per wave
@@ -316,32 +310,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IVC_S2I_WPE
   int32_t* st = reinterpret_cast<int32_t*>(xs) + 4;    // st[-1]: the symbol before the round
   const int64_t nw = (int64_t)gridDim.x * 4;
   bool bad = false;
-  constexpr int NR = SYM_SEG / 256;                    // 16-byte loads per lane per round
-  // a group's bounds are sane (else the general path decides: `bad`)
-  auto sane = [&](int64_t S_, int64_t E_, int nbp_) {
-    return !(S_ < 0 || E_ <= S_ || E_ > z.n || E_ - S_ > (int64_t)nbp_ * 130);
-  };
-  // one round's loads: symbols [s0, s0 + SYM_SEG) of the group and the one after the round
-  auto issue = [&](int64_t S_, int len_, int s0, int j0, int j1, dec_u32x4* v, int& nx) {
-    const __amdgpu_buffer_rsrc_t rs = dec_rsrc(z.sym + S_, (uint32_t)len_ * 4u);
-#pragma unroll
-    for (int j = j0; j < j1; ++j)
-      v[j - j0] = __builtin_amdgcn_raw_buffer_load_b128(rs, (s0 + j * 256 + lane * 4) * 4, 0, 0);
-    nx = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, (s0 + SYM_SEG) * 4, 0, 0);
-  };
-  // the group bounds are loaded one group ahead (scalar loads in flight during the group), and
-  // the next group's first round of symbols is in flight (registers) while this group is
-  // parsed and transformed: a group waits for its stream only when it is longer than a round
+  // the group bounds are loaded one group ahead (scalar loads in flight during the group)
   int64_t g = (int64_t)blockIdx.x * 4 + wave;
   int64_t Sn = g < a.ngroups ? z.gstart[g] : 0, En = g < a.ngroups ? z.gstart[g + 1] : 0;
-  constexpr int PF = IVC_S2I_PF < NR ? IVC_S2I_PF : NR;   // prefetched loads of the first round
-  dec_u32x4 pf[PF > 0 ? PF : 1];
-  int pfx = 0;
-  auto prefetch = [&](int64_t gg, int64_t S_, int64_t E_) {
-    if (PF > 0 && gg < a.ngroups && sane(S_, E_, C * dec_group<DEC_IMAGE>(a, gg).nb))
-      issue(S_, (int)(E_ - S_), 0, 0, PF, pf, pfx);
-  };
-  prefetch(g, Sn, En);
   for (; g < a.ngroups; g += nw) {
     const DecGroup G = dec_group<DEC_IMAGE>(a, g);
     const int64_t S = Sn, E = En;
@@ -350,12 +321,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IVC_S2I_WPE
       En = z.gstart[g + nw + 1];
     }
     const int nbp = C * G.nb;                          // block-planes (EOBs) of the group
-    if (!sane(S, E, nbp)) {
+    if (S < 0 || E <= S || E > z.n || E - S > (int64_t)nbp * 130) {
       bad = true;                                      // wave-uniform
-      prefetch(g + nw, Sn, En);
       continue;
     }
     const int len = (int)(E - S);
+    const __amdgpu_buffer_rsrc_t rs = dec_rsrc(z.sym + S, (uint32_t)len * 4u);
     // zero the coefficient staging (C x 8 rows of SYM_QP int16)
 #pragma unroll
     for (int j = 0; j < (QS / 8 + 63) / 64; ++j) {
@@ -368,26 +339,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IVC_S2I_WPE
     int prevc = 1;          // the symbol before the round (a group starts at a value slot)
     for (int s0 = 0; s0 < len; s0 += SYM_SEG) {
       // one round: every load in flight, then the LDS writes
-      dec_u32x4 v[NR];
-      int nxt;
-      if (s0 == 0 && PF > 0) {
-        if (PF < NR) issue(S, len, 0, PF, NR, v + PF, nxt);
+      dec_u32x4 v[SYM_SEG / 256];
 #pragma unroll
-        for (int j = 0; j < PF; ++j) v[j] = pf[j];
-        if (PF == NR) nxt = pfx;
-      } else {
-        issue(S, len, s0, 0, NR, v, nxt);
-      }
+      for (int j = 0; j < SYM_SEG / 256; ++j)
+        v[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, (s0 + j * 256 + lane * 4) * 4, 0, 0);
+      const int nxt = (int)__builtin_amdgcn_raw_buffer_load_b32(rs, (s0 + SYM_SEG) * 4, 0, 0);
       __builtin_amdgcn_wave_barrier();                 // the previous round's reads are done
 #pragma unroll
-      for (int j = 0; j < NR; ++j)
+      for (int j = 0; j < SYM_SEG / 256; ++j)
         *reinterpret_cast<dec_u32x4*>(st + j * 256 + lane * 4) = v[j];
       if (lane == 0) {
         st[-1] = prevc;
         st[SYM_SEG] = nxt;
       }
       __builtin_amdgcn_wave_barrier();
-      if (s0 == 0) prefetch(g + nw, Sn, En);          // the next group's first round
       const int rlen = len - s0 < SYM_SEG ? len - s0 : SYM_SEG;
       for (int c0 = 0; c0 < rlen; c0 += 64) {
         const int i = c0 + lane;

@@ -490,105 +490,6 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
   }
 }
 
-// The emit pass with lane = coefficient (IVC_ZW_LANE, the default): the group's 16 blocks
-// arrive as the same 16-byte loads, go through the wave's LDS once (4 ds_write_b128 per lane)
-// and come back as one register per block with lane i = coefficient i, and then each block is
-// emitted as the fused encoder's emission does it (ivc_kernels.hip zr_group_emit_fit): its
-// nonzero mask is one ballot, the run starts two scalar mask operations on it (previous lane
-// nonzero: m << 1 | 1; a nonzero at or after the lane: the ballot of m >> lane != 0), each
-// lane's slot two mbcnt, and two ds_write per lane at one address.  Per block: ~20 VALU and a
-// dozen scalar instructions instead of the per-nibble mask algebra of the 4-coefficient lanes;
-// the staged writes of a dense block are lane-consecutive (no 4-word stride, so no bank
-// conflicts).  The block offsets leave as one 16-lane store per group.
-#ifndef IVC_ZW_LANE
-#define IVC_ZW_LANE 1
-#endif
-__global__ __launch_bounds__(256) void zw_emit_lane_kernel(const int32_t* __restrict__ src, int64_t nblk,
-                                                           int32_t eob, const int64_t* __restrict__ goff,
-                                                           int64_t* __restrict__ off,
-                                                           int32_t* __restrict__ out, int64_t capacity) {
-  __shared__ __attribute__((aligned(16))) int32_t stage[4 * ZW_STAGE_D];
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  int32_t* const zbase = stage + (threadIdx.x >> 6) * ZW_STAGE_D;
-  int32_t* const dummy = zbase + ZW_STAGE + 4 + lane;
-  constexpr int EG = IVC_ZW_EMIT_GROUPS;
-  for (int64_t b00 = wave * ZW_BLK * EG; b00 < nblk; b00 += nw * ZW_BLK * EG) {
-    zv4 xx[EG * ZW_LOADS];
-#pragma unroll
-    for (int u = 0; u < EG * ZW_LOADS; ++u) xx[u] = zw_load(src, nblk, b00, u, lane);
-#pragma unroll
-    for (int gg = 0; gg < EG; ++gg) {
-      const int64_t b0 = b00 + gg * ZW_BLK;
-      if (b0 >= nblk) break;                                        // wave-uniform
-      const int64_t g = b0 / ZW_BLK;
-      const int64_t wbase = goff[g], wend = goff[g + 1];
-      // transpose: load u's lane l holds coefficients 4 (l % 16) .. of block 4 u + l / 16, which
-      // is word 64 (4 u + l / 16) + 4 (l % 16) of the group = 4 (16 u + l)
-#pragma unroll
-      for (int u = 0; u < ZW_LOADS; ++u)
-        *reinterpret_cast<zv4*>(zbase + 4 * (16 * u + lane)) = xx[gg * ZW_LOADS + u];
-      __builtin_amdgcn_wave_barrier();
-      int32_t xb[ZW_BLK];
-#pragma unroll
-      for (int b = 0; b < ZW_BLK; ++b) xb[b] = zbase[64 * b + lane];
-      __builtin_amdgcn_wave_barrier();                              // the region becomes the window
-      const int sh = IVC_ZW_STORE4 ? (int)(((uintptr_t)(out + wbase) >> 2) & 3u) : 0;
-      int32_t* const zs = zbase + sh;
-      const int nlive = nblk - b0 < ZW_BLK ? (int)(nblk - b0) : ZW_BLK;
-      int fill = 0;
-      int fills = 0;                                                // lane b: block b's offset
-#pragma unroll
-      for (int b = 0; b < ZW_BLK; ++b) {
-        if (b >= nlive) break;                                      // wave-uniform
-        fills = lane == b ? fill : fills;
-        const int32_t x = xb[b];
-        const bool nz = x != 0;
-        const uint64_t m = __ballot(nz);
-        const uint64_t later = m >> lane;                           // this lane's bit and above
-        const uint64_t pm = (m << 1) | 1ull, hm = __ballot(later != 0);
-        const uint64_t st = pm & hm & ~m;                           // run starts before the last nonzero
-        const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
-        const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
-                        2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
-        // a nonzero, a run's 0 + its length, or (the first zero after the last nonzero) the EOB
-        const bool w1 = __builtin_amdgcn_inverse_ballot_w64(m | pm);
-        const int32_t v1 = __builtin_amdgcn_inverse_ballot_w64(m | hm) ? x : eob;
-        const int32_t v2 = __builtin_amdgcn_inverse_ballot_w64(st) ? (int32_t)__builtin_ctzll(later) : eob;
-        int32_t* const d = w1 ? zs + fill + pos : dummy;
-        d[1] = v2;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");     // keep the two writes ordered
-        d[0] = v1;
-        fill += cnt;
-      }
-      if (lane < nlive) off[b0 + lane] = wbase + fills;             // the block offsets
-      __builtin_amdgcn_wave_barrier();
-      const int n = (int)(wend - wbase);
-#if IVC_ZW_STORE4
-      const int64_t A = wbase - sh;
-      const int nq = (sh + n + 3) >> 2;
-      for (int t = lane; t < nq; t += 64) {
-        const int w0 = 4 * t;
-        const int64_t ga = A + w0;
-        if (w0 >= sh && w0 + 4 <= sh + n && ga + 4 <= capacity) {
-          *reinterpret_cast<zv4*>(out + ga) = *reinterpret_cast<const zv4*>(zbase + w0);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            if (w0 + e >= sh && w0 + e < sh + n && ga + e < capacity) out[ga + e] = zbase[w0 + e];
-        }
-      }
-#else
-      const int64_t lim = capacity - wbase;
-      for (int k = lane; k < n; k += 64)
-        if (k < lim) out[wbase + k] = zs[k];
-#endif
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-}
-
 static bool zw_ok(const int32_t* src, int stride, int B) {
   return stride == 64 && B == 64 && ((uintptr_t)src & 15u) == 0;
 }
@@ -675,12 +576,8 @@ hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int
   if (nblk <= 0) return hipSuccess;
   if (zw_ok(src, stride, B)) {
     const ZrScratch z = zr_scratch(scratch, nblk);
-    if (IVC_ZW_LANE)
-      zw_emit_lane_kernel<<<zw_grid((nblk + IVC_ZW_EMIT_GROUPS - 1) / IVC_ZW_EMIT_GROUPS, 6), 256, 0, s>>>(
-          src, nblk, eob, z.goff, off, out, capacity);
-    else
-      zw_emit_kernel<<<zw_grid((nblk + IVC_ZW_EMIT_GROUPS - 1) / IVC_ZW_EMIT_GROUPS, 6), 256, 0, s>>>(
-          src, nblk, eob, z.goff, off, out, capacity);
+    zw_emit_kernel<<<zw_grid((nblk + IVC_ZW_EMIT_GROUPS - 1) / IVC_ZW_EMIT_GROUPS, 6), 256, 0, s>>>(
+        src, nblk, eob, z.goff, off, out, capacity);
   } else {
     zr_emit_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, eob, off, out, capacity);
   }

@@ -374,6 +374,17 @@ struct FusedArgs {
   // exchange needs no pass over the stream
   unsigned long long* zr_hist;
   int32_t zr_hist_lo, zr_hist_n;
+  // OUT_COUNT hand-off to the symbol emitter (sym_emit_kernel): the group's quantised
+  // coefficients by zig-zag position (lane) as int8 [gid][64][c8_stride], and as int16
+  // [gid][64][2 c8_stride] for a group with a value outside int8 (zr_cflag[gid] = 1)
+  int8_t* zr_c8;
+  int16_t* zr_c16;
+  uint8_t* zr_cflag;
+  // a value outside int16 anywhere: *zr_cbad = 1, and the fused emission pass (which redoes the
+  // transform) runs instead of the emitter: each kernel reads the word first (zr_gate: run
+  // only when *zr_gate != 0)
+  int* zr_cbad;
+  const int* zr_gate;
   // store pacing (OUT_COEFS): slot s of wave w (of W) stores no earlier than
   // (*pace_t0 + (s * pace_d + w * pace_d / W) / 256) on the 100 MHz s_memrealtime clock;
   // pace_d = 0: unpaced
@@ -780,6 +791,9 @@ constexpr int ZR_WIN = XS_PITCH * 8 * 8 / 4;   // int32 symbols in a wave's tran
 #ifndef IVC_EMIT_FIT
 #define IVC_EMIT_FIT 1                           // 0: every group through the general emission
 #endif
+#ifndef IVC_EMIT_C8
+#define IVC_EMIT_C8 1                            // emitter from the count pass's int8 hand-off
+#endif
 #ifndef IVC_EMIT_MASK
 #define IVC_EMIT_MASK 1                          // fit path: run starts from scalar lane masks (0: DPP)
 #endif
@@ -979,19 +993,15 @@ __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* o
   __builtin_amdgcn_wave_barrier();
 }
 
+// A group's emission from its coefficients in registers (xv[b][p] = zig-zag position `lane`
+// of block b, plane p) into the wave's window `os` (ZR_WIN words), then the stream.
 template <int C, bool DUP, bool HIST>
-__device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, int nb,
-                                              int64_t gbase, int gcount, ZrHistAcc& H) {
-  constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging
-  constexpr int PITCH = os_pitch<C, DUP>();
+__device__ __forceinline__ void zr_emit_regs(const FusedArgs& a, int32_t* os, int nb, int64_t gbase,
+                                             int gcount,
+                                             const int32_t (&xv)[8][(C == 1 && DUP) ? 2 : 3],
+                                             ZrHistAcc& H) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;
   const int lane = threadIdx.x & 63;
-  const int ra = sym_read_addr(lane);           // zig-zag position `lane` in the swizzled staging
-  int32_t xv[8][NP];
-#pragma unroll
-  for (int b = 0; b < 8; ++b)
-#pragma unroll
-    for (int p = 0; p < NP; ++p) xv[b][p] = os[b * PITCH + p * 64 + ra];
-  __builtin_amdgcn_wave_barrier();              // staging read: the region becomes the window
   if (IVC_EMIT_FIT && nb == 8 && gcount <= ZR_WIN - 65) {
     zr_group_emit_fit<C, DUP, HIST>(a, os, gbase, gcount, xv, H);
     return;
@@ -1070,6 +1080,77 @@ __device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, i
   flush();
 }
 
+template <int C, bool DUP, bool HIST>
+__device__ __forceinline__ void zr_group_emit(const FusedArgs& a, int32_t* os, int nb,
+                                              int64_t gbase, int gcount, ZrHistAcc& H) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;   // distinct planes in the staging
+  constexpr int PITCH = os_pitch<C, DUP>();
+  const int lane = threadIdx.x & 63;
+  const int ra = sym_read_addr(lane);           // zig-zag position `lane` in the swizzled staging
+  int32_t xv[8][NP];
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+#pragma unroll
+    for (int p = 0; p < NP; ++p) xv[b][p] = os[b * PITCH + p * 64 + ra];
+  __builtin_amdgcn_wave_barrier();              // staging read: the region becomes the window
+  zr_emit_regs<C, DUP, HIST>(a, os, nb, gbase, gcount, xv, H);
+}
+
+// The count pass's hand-off (a.zr_c8): lane k gathers zig-zag position k of the group's 8
+// blocks x NP planes from the staging (lane-consecutive reads) and stores them as int8 — one
+// 16-byte store per lane for NP = 2 — or, when any value of the group lies outside int8, as
+// int16 in the group's slot of a.zr_c16 (flag 1).  The emitter then needs neither the pixels
+// nor the transform.
+constexpr int c8_stride(int NP) { return NP == 2 ? 16 : 32; }    // bytes per lane (>= 8 NP)
+template <int C, bool DUP>
+__device__ __forceinline__ void zr_export_coefs(const FusedArgs& a, const int32_t* os, int64_t gid) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;
+  constexpr int PITCH = os_pitch<C, DUP>();
+  constexpr int S8 = c8_stride(NP);
+  const int lane = threadIdx.x & 63;
+  int32_t v[8 * NP];
+  bool wide = false, wider = false;
+#pragma unroll
+  for (int b = 0; b < 8; ++b)
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const int32_t x = os[b * PITCH + p * 64 + lane];
+      v[b * NP + p] = x;
+      wide |= (uint32_t)(x + 128) > 255u;
+      wider |= (uint32_t)(x + 32768) > 65535u;
+    }
+  if (__ballot(wider) && lane == 0) atomicOr(a.zr_cbad, 1);
+  uint32_t w8[S8 / 4];
+#pragma unroll
+  for (int k = 0; k < S8 / 4; ++k) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (4 * k + e < 8 * NP) d |= ((uint32_t)v[4 * k + e] & 0xffu) << (8 * e);
+    w8[k] = d;
+  }
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4* d8 = reinterpret_cast<u32x4*>(a.zr_c8 + (gid * 64 + lane) * S8);
+#pragma unroll
+  for (int k = 0; k < S8 / 16; ++k) d8[k] = u32x4{w8[4 * k], w8[4 * k + 1], w8[4 * k + 2], w8[4 * k + 3]};
+  const bool any_wide = __ballot(wide) != 0;
+  if (lane == 0) a.zr_cflag[gid] = any_wide ? 1 : 0;
+  if (any_wide) {                                             // wave-uniform, rare
+    uint32_t w16[S8 / 2];
+#pragma unroll
+    for (int k = 0; k < S8 / 2; ++k) {
+      const int e0 = 2 * k, e1 = 2 * k + 1;
+      const uint32_t lo = e0 < 8 * NP ? ((uint32_t)v[e0] & 0xffffu) : 0u;
+      const uint32_t hi = e1 < 8 * NP ? ((uint32_t)v[e1] & 0xffffu) : 0u;
+      w16[k] = lo | hi << 16;
+    }
+    u32x4* d16 = reinterpret_cast<u32x4*>(a.zr_c16 + (gid * 64 + lane) * S8);
+#pragma unroll
+    for (int k = 0; k < S8 / 8; ++k)
+      d16[k] = u32x4{w16[4 * k], w16[4 * k + 1], w16[4 * k + 2], w16[4 * k + 3]};
+  }
+}
+
 // OUT_COUNT: the group's symbol count from the zig-zag staging.  Lane (b, r) takes zig-zag
 // positions 8r .. 8r+7 of block b; a block's nonzero mask is the OR of its 8 lanes' bytes.
 template <int C, bool DUP, int OUTM>
@@ -1111,6 +1192,7 @@ __device__ __forceinline__ void zr_group(const FusedArgs& a, int32_t* os, int b,
     st[p] = zeros & ~(zeros << 1);
     cnt[p] = live ? __builtin_popcountll(lm) + 2 * __builtin_popcountll(st[p]) + 1 : 0;
   }
+  if (a.zr_c8) zr_export_coefs<C, DUP>(a, os, gid);
   __builtin_amdgcn_wave_barrier();                            // staging read: region free
   const int tb = cnt[0] + cnt[1] + cnt[NP - 1];               // the block's symbols
   int v = 0;                                                  // lane 8b holds block b's total
@@ -1152,6 +1234,7 @@ __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && 
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   const int b = lane >> 3, r = lane & 7;
+  if (a.zr_gate && *a.zr_gate == 0) return;           // (the emitter's fallback, not needed)
   for (int i = tid; i < 192; i += 256) {
     sq[i] = (D)t.q[i];
     // s_i * s_k * RN(1/q): the DCT's power-of-two output scales folded into the reciprocal
@@ -1754,7 +1837,9 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
   auto go = [&](auto k) {
     const unsigned g = grid(k);
     const int64_t nw = 4 * (int64_t)g;
-    const int slot = setup_pacing(a, kind, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
+    // the luma-only variant runs unpaced: its PMC (profiles/r04g_pmc_luma.json) shows it
+    // issue-bound, not store-order-bound, and faster without the schedule
+    const int slot = OUTM == OUT_LUMA ? -1 : setup_pacing(a, kind, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
     k<<<g, 256, 0, s>>>(a, t);
     finish_pacing(kind, slot, s);
   };
@@ -1802,6 +1887,11 @@ static FusedArgs make_fused_args(const void* img, const int64_t* mv, int32_t* ou
   a.zr_hist = nullptr;
   a.zr_hist_lo = 0;
   a.zr_hist_n = 0;
+  a.zr_c8 = nullptr;
+  a.zr_c16 = nullptr;
+  a.zr_cflag = nullptr;
+  a.zr_cbad = nullptr;
+  a.zr_gate = nullptr;
   a.pace_t0 = nullptr;
   a.pace_d = 0;
   a.pace_early = 0;
@@ -1867,6 +1957,65 @@ hipError_t launch_intra_encode_luma(const uint8_t* img, int64_t nframes, int64_t
 
 // ---- pixels -> zero-run symbols (IntraCodec.image2symbols' hot part, intracodec.py:66-81):
 // count pass, int64 scan of the per-group counts, emission pass.
+// The symbol emitter of the two-pass pixels -> symbols path (IVC_EMIT_C8): group gid's
+// coefficients come from the count pass's hand-off (int8, or int16 for a group flagged wide),
+// not from the pixels, so the pass is the emission alone — no pixel loads, no transform.
+// One wave per group (grid-stride); the window and the histogram bins as in the fused pass.
+// Exits at once when the count pass met a value outside int16 (*zr_cbad): the fused emission
+// pass runs instead.
+template <int C, bool DUP, bool HIST, int NG>
+__global__ __launch_bounds__(256) void sym_emit_kernel(FusedArgs a, int64_t ngroups) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;
+  constexpr int S8 = c8_stride(NP);
+  __shared__ __attribute__((aligned(16))) int32_t win[4 * ZR_WIN];
+  __shared__ uint32_t zh[HIST ? ZH_LDS : 1];
+  if (*a.zr_cbad) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  ZrHistAcc hacc{nullptr};
+  if constexpr (HIST) {
+    for (int i = tid; i < ZH_LDS; i += 256) zh[i] = 0;
+    hacc.bins = zh;
+    __syncthreads();
+  }
+  int32_t* os = win + wave * ZR_WIN;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  for (int64_t gid = (int64_t)blockIdx.x * 4 + wave; gid < ngroups; gid += nw) {
+    const int gcount = a.zr_counts[gid];
+    if (gcount == 0) continue;                                   // a group past the row's end
+    const int64_t gbase = a.zr_off[gid];
+    const int nb = group_loc<NG>(a, (uint32_t)(gid / NG), (int)(gid % NG)).nb;
+    int32_t xv[8][NP];
+    if (a.zr_cflag[gid] == 0) {
+      const i32x4* src = reinterpret_cast<const i32x4*>(a.zr_c8 + (gid * 64 + lane) * S8);
+      i32x4 w[S8 / 16];
+#pragma unroll
+      for (int k = 0; k < S8 / 16; ++k) w[k] = __builtin_nontemporal_load(src + k);
+#pragma unroll
+      for (int e = 0; e < 8 * NP; ++e) {
+        const uint32_t word = (uint32_t)w[e / 16][(e / 4) & 3];
+        xv[e / NP][e % NP] = (int32_t)(int8_t)(uint8_t)(word >> (8 * (e & 3)));
+      }
+    } else {
+      const i32x4* src = reinterpret_cast<const i32x4*>(a.zr_c16 + (gid * 64 + lane) * S8);
+      i32x4 w[S8 / 8];
+#pragma unroll
+      for (int k = 0; k < S8 / 8; ++k) w[k] = src[k];
+#pragma unroll
+      for (int e = 0; e < 8 * NP; ++e) {
+        const uint32_t word = (uint32_t)w[e / 8][(e / 2) & 3];
+        xv[e / NP][e % NP] = (int32_t)(int16_t)(uint16_t)(word >> (16 * (e & 1)));
+      }
+    }
+    zr_emit_regs<C, DUP, HIST>(a, os, nb, gbase, gcount, xv, hacc);
+  }
+  if constexpr (HIST) {
+    __syncthreads();
+    zh_flush(a, zh, tid);
+  }
+}
+
 template <typename TI, int C, bool DUP, bool CM, int OUTM>
 static void launch_fused_zr(const FusedArgs& a_in, const QTab& t, hipStream_t s) {
   constexpr int NG = (sizeof(TI) == 1 && C == 1) ? IVC_WIDE_NG : 1;
@@ -1887,17 +2036,44 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
   int32_t* counts = nullptr;
   int64_t* agg = nullptr;
   int64_t* off = nullptr;
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;
+  // the coefficient hand-off (IVC_EMIT_C8): only when the stream is emitted
+  const bool c8 = IVC_EMIT_C8 && a.zr_cap > 0;
+  int8_t* c8buf = nullptr;
+  int16_t* c16buf = nullptr;
+  uint8_t* cflag = nullptr;
+  int* cbad = nullptr;
   hipError_t e = scratch_alloc((void**)&counts, (size_t)ngroups * 4, s);
   if (e == hipSuccess) e = scratch_alloc((void**)&agg, (size_t)scan_scratch_elems(ngroups) * 8, s);
   if (e == hipSuccess) e = scratch_alloc((void**)&off, (size_t)(ngroups + 1) * 8, s);
+  if (c8) {
+    const size_t per = (size_t)64 * c8_stride(NP);
+    if (e == hipSuccess) e = scratch_alloc((void**)&c8buf, (size_t)ngroups * per, s);
+    if (e == hipSuccess) e = scratch_alloc((void**)&c16buf, (size_t)ngroups * 2 * per, s);
+    if (e == hipSuccess) e = scratch_alloc((void**)&cflag, (size_t)ngroups + 16, s);
+    if (e == hipSuccess) e = scratch_alloc((void**)&cbad, 16, s);
+    if (e == hipSuccess) e = hipMemsetAsync(cbad, 0, 16, s);
+  }
   if (e == hipSuccess) {
     a.zr_counts = counts;
     a.zr_off = off;
+    a.zr_c8 = c8buf;
+    a.zr_c16 = c16buf;
+    a.zr_cflag = cflag;
+    a.zr_cbad = cbad;
     launch_fused_zr<TI, C, DUP, CM, OUT_COUNT>(a, t, s);
     e = launch_exclusive_scan_i32(counts, ngroups, agg, off, s);
   }
   if (e == hipSuccess) e = hipMemcpyAsync(nsym, off + ngroups, 8, hipMemcpyDeviceToDevice, s);
   if (e == hipSuccess && a.zr_cap > 0) {
+    if (c8) {
+      // the emitter; the fused emission pass only when the emitter stood down (*cbad)
+      auto k = a.zr_hist ? sym_emit_kernel<C, DUP, true, NG> : sym_emit_kernel<C, DUP, false, NG>;
+      FusedArgs ae = a;
+      ae.tpr = (int)tpr;                  // group_loc's tiles of NG groups, as the count pass
+      k<<<resident_grid(k, (ngroups + 3) / 4), 256, 0, s>>>(ae, ngroups);
+      a.zr_gate = cbad;
+    }
     if (a.zr_hist) launch_fused_zr<TI, C, DUP, CM, OUT_SYMH>(a, t, s);
     else launch_fused_zr<TI, C, DUP, CM, OUT_SYMBOLS>(a, t, s);
     e = hipGetLastError();
@@ -1905,6 +2081,8 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
   if (counts) (void)hipFreeAsync(counts, s);
   if (agg) (void)hipFreeAsync(agg, s);
   if (off) (void)hipFreeAsync(off, s);
+  for (void* pp : {(void*)c8buf, (void*)c16buf, (void*)cflag, (void*)cbad})
+    if (pp) (void)hipFreeAsync(pp, s);
   return e;
 }
 

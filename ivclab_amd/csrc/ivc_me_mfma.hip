@@ -67,11 +67,8 @@ __host__ __device__ constexpr int wave_dy0(int w) { return 8 * w; }
 __host__ __device__ constexpr int wave_ndy(int w) { return w == 3 ? 9 : 8; }
 }  // namespace mf
 
-#ifndef IVC_ME_SWP
-#define IVC_ME_SWP 1         // software-pipelined M-tiles (0: operands read at each M-tile)
-#endif
-#ifndef IVC_ME_SWP_R
-#define IVC_ME_SWP_R 4       // rows (and E words) of the next M-tile read ahead
+#ifndef IVC_ME_2ROW
+#define IVC_ME_2ROW 1        // two block rows per tile (me_mfma16x2_kernel); 0: one block row
 #endif
 
 typedef int mf_v4i __attribute__((ext_vector_type(4)));
@@ -262,84 +259,6 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
     mf_v4i bk = rot(bop, std::integral_constant<int, 0x93>{});   // r = 3: quads 3, 0, 1, 2
     mf_v4i bks = mf_v4i{bk.z, bk.w, bk.x, bk.y};      // block rows 2g + 1 | 2g
     int acc0 = INT_MIN, acc1 = INT_MIN;                 // running best key of quads k - 1, k
-#if IVC_ME_SWP
-    // software-pipelined M-tiles: M-tile mt + 1's operands (10 reference rows and 9 E words
-    // per lane) are read from LDS while M-tile mt's MFMAs run, so the steps never wait on LDS
-    // latency.  Every wave runs a ninth step (dy = dyw0 + 8) so that an M-tile is one basic
-    // block; in waves 0-2 (8 dy each) its C operand masks every output (below VALID_MIN).
-    // (the first SWP_R rows and E words of an M-tile are prefetched; the rest are read at the
-    // M-tile's start, ahead of the steps that need them)
-    constexpr int PR = IVC_ME_SWP_R < 10 ? IVC_ME_SWP_R : 10, PE = PR < 9 ? PR : 9;
-    struct MtOps {
-      mf_u32x2 r[PR];                                   // rows dyw0 + 2g + kk, bytes u .. u+7
-      int e[PE];                                        // E[dyw0 + d][u]
-    };
-    auto row_at = [&](int mt, int kk) {
-      const int wd = 4 * mt + (l16 >> 2);               // word of window position u = 16 mt + l16
-      const int rr = dyw0 + 2 * g + kk;
-      return mf_u32x2{cb[rr * PITCH + wd], cb[rr * PITCH + wd + 1]};
-    };
-    auto load_mt = [&](int mt, MtOps& L) {
-#pragma unroll
-      for (int kk = 0; kk < PR; ++kk) L.r[kk] = row_at(mt, kk);
-#pragma unroll
-      for (int d = 0; d < PE; ++d) L.e[d] = ev[16 * mt + d * U];
-    };
-    // the window operand of step dl is rows (dl, dl + 1): one 4-dword tuple T = [P | Q] serves
-    // every step without register copies (step dl + 1 overwrites the half holding row dl with
-    // row dl + 2, and odd steps use the block operand with its halves swapped)
-    auto do_mt = [&](int mt, const MtOps& L, int q0, int q1, const mf_v4i& bk, const mf_v4i& bks) {
-      mf_u32x2 rt[10 - PR > 0 ? 10 - PR : 1];
-      int et[9 - PE > 0 ? 9 - PE : 1];
-#pragma unroll
-      for (int kk = PR; kk < 10; ++kk) rt[kk - PR] = row_at(mt, kk);
-#pragma unroll
-      for (int d = PE; d < 9; ++d) et[d - PE] = ev[16 * mt + d * U];
-      auto rowv = [&](int kk) { return kk < PR ? L.r[kk < PR ? kk : 0] : rt[kk >= PR ? kk - PR : 0]; };
-      auto ev_ = [&](int d) { return d < PE ? L.e[d < PE ? d : 0] : et[d >= PE ? d - PE : 0]; };
-      const int v0 = 16 * mt + cj - 32 * q0, v1 = 16 * mt + cj - 32 * q1;
-      const mf_v4i cm = mf_v4i{(unsigned)v0 <= 32u ? 0 : MASK_C, (unsigned)v1 <= 32u ? 0 : MASK_C, 0, 0};
-      const mf_v4i cm8 = wave == 3 ? cm : mf_v4i{MASK_C, MASK_C, 0, 0};
-      mf_v4i T;
-      {
-        const mf_u32x2 r0 = rowv(0), r1 = rowv(1);
-        T = mf_v4i{(int)r0.x, (int)r0.y, (int)r1.x, (int)r1.y};
-      }
-#pragma unroll
-      for (int dl = 0; dl < 9; ++dl) {
-        if (dl > 0) {
-          const mf_u32x2 rn = rowv(dl + 1);
-          if (dl & 1) {
-            T.x = (int)rn.x;
-            T.y = (int)rn.y;
-          } else {
-            T.z = (int)rn.x;
-            T.w = (int)rn.y;
-          }
-        }
-        const mf_v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8((dl & 1) ? bks : bk, T,
-                                                               dl == 8 ? cm8 : cm, 0, 0, 0);
-        const uint32_t e = (uint32_t)ev_(dl);
-        acc0 = max(acc0, (int)(((uint32_t)d.x << 8) + e));
-        acc1 = max(acc1, (int)(((uint32_t)d.y << 8) + e));
-      }
-    };
-    MtOps LA, LB;
-    load_mt(0, LA);
-#pragma unroll 1
-    for (int k = 0; k < NMT / 2; ++k) {
-      const int q0 = (k + 3) & 3, q1 = k & 3;
-      load_mt(2 * k + 1, LB);
-      do_mt(2 * k, LA, q0, q1, bk, bks);
-      load_mt(2 * k + 2 < NMT ? 2 * k + 2 : NMT - 1, LA);
-      do_mt(2 * k + 1, LB, q0, q1, bk, bks);
-      if (k > 0) finish(q0, acc0);                      // quad k - 1 is complete
-      acc0 = acc1;
-      acc1 = INT_MIN;
-      bk = rot(bk, std::integral_constant<int, 0x39>{});  // r + 1: quad_perm 1,2,3,0
-      bks = mf_v4i{bk.z, bk.w, bk.x, bk.y};
-    }
-#else
 #pragma unroll 1
     for (int k = 0; k < NMT / 2; ++k) {
       const int q0 = (k + 3) & 3, q1 = k & 3;
@@ -397,7 +316,6 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
       bk = rot(bk, std::integral_constant<int, 0x39>{});  // r + 1: quad_perm 1,2,3,0
       bks = mf_v4i{bk.z, bk.w, bk.x, bk.y};
     }
-#endif
     __syncthreads();
     if (tid < TB) {
       const int j = tid, bx = bx0 + j;
@@ -415,12 +333,290 @@ __global__ __launch_bounds__(256, 3) void me_mfma16_kernel(const uint8_t* __rest
   }
 }
 
+// ---- two block rows per tile (IVC_ME_2ROW) --------------------------------------------------
+// A tile is 8 adjacent blocks of block row by (top) and the 8 below them (bottom): 16 MFMA
+// rows.  The bottom blocks' windows at dy' are the top blocks' windows at dy = dy' + 8 (the
+// same reference rows), so one MFMA over the reference rows at offset R (R in [0, 40], rows
+// yb + R .. of yb = 8 by - 16) serves the top blocks' candidates dy = R and the bottom blocks'
+// dy' = R - 8.  Against one block row of 16: the window positions per tile drop from 160 to
+// 96 (6 M-tiles), MFMAs per 16 blocks from 330 to 246, key formations from 660 to 528 register
+// operations (a register is a quad of blocks: top 0-3, top 4-7, bottom 0-3, bottom 4-7, and a
+// quad is live in 4 of the 6 M-tiles and for 33 of the 41 offsets R), and the LDS from 51.7 KB
+// to 39.4 KB: 4 workgroups per CU instead of 3.  Ties and keys as in me_mfma16_kernel: rank =
+// (R - the wave's first R) * 6 + mt orders a lane's candidates of a block in raster order.
+namespace mf2 {
+constexpr int SR = 16, N = 2 * SR + 1, TBX = 8;   // blocks per tile row
+constexpr int NR = 41;                             // offsets R
+constexpr int ROWS = 48;                           // staged reference rows
+constexpr int U = 96, NMT = U / 16;                // window positions, M-tiles
+constexpr int NPAIR = 13;                          // staged 8-byte pairs per row (104 bytes)
+constexpr int PITCH = 30;                          // dwords per copy row (26 + 1 used); 2 PITCH = 28 mod 32
+constexpr int ITEMS = ROWS * NPAIR;
+constexpr int IPT = (ITEMS + 255) / 256;
+constexpr int COPY = 1448;                         // >= ROWS * PITCH, = 8 mod 32
+static_assert(COPY >= ROWS * PITCH && COPY % 32 == 8 && (2 * PITCH) % 8 == 4, "bank layout");
+constexpr int E_OFF = 4 * COPY;                    // E[R][u]
+constexpr int RED_OFF = E_OFF + NR * U;
+constexpr int LDS_DW = RED_OFF + 4 * 16 * 2;
+static_assert(LDS_DW * 4 <= 40960, "4 workgroups per CU");
+// wave w: offsets [r0, r0 + nr): 11, 10, 10, 10
+__host__ __device__ constexpr int wave_r0(int w) { return w == 0 ? 0 : 10 * w + 1; }
+__host__ __device__ constexpr int wave_nr(int w) { return w == 0 ? 11 : 10; }
+}  // namespace mf2
+
+template <int WV>    // 0: wave 0, 1: waves 1 and 2, 3: wave 3 (liveness of the halves by R)
+__device__ __forceinline__ void me2_search(const uint32_t* lds, int* red, int wave, int g, int l16,
+                                           mf_v4i bop) {
+  using namespace mf2;
+  using mf::MASK_C;
+  using mf::VALID_MIN;
+  const int r0 = wave_r0(wave);
+  constexpr int NRW = WV == 0 ? 11 : 10;
+  const uint32_t* cb = lds + (l16 & 3) * COPY;
+  const int* ev = reinterpret_cast<const int*>(lds + E_OFF) + l16 + r0 * U;
+  // block operand rows: register i (D row 4g + i) holds quad i = (i >> 1 ? bottom : top),
+  // blocks 4 (i & 1) .. + 3, lane group g = block 4 (i & 1) + g of it
+  const mf_v4i bks = mf_v4i{bop.z, bop.w, bop.x, bop.y};
+  int acc[4] = {INT_MIN, INT_MIN, INT_MIN, INT_MIN};
+  // quads 0 / 2 (blocks 0-3) serve M-tiles 0-3, quads 1 / 3 (blocks 4-7) M-tiles 2-5: three
+  // segments of two M-tiles with the live quads fixed at compile time, each M-tile one basic
+  // block (a fully unrolled search lets the scheduler hoist every LDS read: spills)
+  auto mtile = [&](int mt, auto q01c, auto q23c) {
+    constexpr bool q01 = decltype(q01c)::value, q23 = decltype(q23c)::value;
+    const int wd = 4 * mt + (l16 >> 2);
+    const int v0 = 16 * mt + l16 - 8 * g, v1 = v0 - 32;          // u - 8 j for j = g, 4 + g
+    const int c0 = (unsigned)v0 <= 32u ? 0 : MASK_C, c1 = (unsigned)v1 <= 32u ? 0 : MASK_C;
+    const mf_v4i cm = mf_v4i{c0, c1, c0, c1};
+    auto row = [&](int kk) {
+      const int rr = r0 + 2 * g + kk;
+      return mf_u32x2{cb[rr * PITCH + wd], cb[rr * PITCH + wd + 1]};
+    };
+    mf_v4i T;
+    {
+      const mf_u32x2 a0 = row(0), a1 = row(1);
+      T = mf_v4i{(int)a0.x, (int)a0.y, (int)a1.x, (int)a1.y};
+    }
+#pragma unroll
+    for (int dl = 0; dl < NRW; ++dl) {
+      if (dl > 0) {
+        const mf_u32x2 rn = row(dl + 1);
+        if (dl & 1) {
+          T.x = (int)rn.x;
+          T.y = (int)rn.y;
+        } else {
+          T.z = (int)rn.x;
+          T.w = (int)rn.y;
+        }
+      }
+      const uint32_t e = (uint32_t)ev[dl * U + 16 * mt];
+      const mf_v4i d = __builtin_amdgcn_mfma_i32_16x16x64_i8((dl & 1) ? bks : bop, T, cm, 0, 0, 0);
+      // R = r0 + dl: top live for R <= 32, bottom for R >= 8 (compile time except waves 1-2,
+      // where both always are)
+      const bool top = WV == 0 ? true : (WV == 3 ? dl <= 1 : true);
+      const bool bot = WV == 0 ? dl >= 8 : true;
+      if (top && q01) acc[0] = max(acc[0], (int)(((uint32_t)d.x << 8) + e));
+      if (top && q23) acc[1] = max(acc[1], (int)(((uint32_t)d.y << 8) + e));
+      if (bot && q01) acc[2] = max(acc[2], (int)(((uint32_t)d.z << 8) + e));
+      if (bot && q23) acc[3] = max(acc[3], (int)(((uint32_t)d.w << 8) + e));
+    }
+  };
+#pragma unroll 1
+  for (int mt = 0; mt < 2; ++mt) mtile(mt, std::true_type{}, std::false_type{});
+#pragma unroll 1
+  for (int mt = 2; mt < 4; ++mt) mtile(mt, std::true_type{}, std::true_type{});
+#pragma unroll 1
+  for (int mt = 4; mt < NMT; ++mt) mtile(mt, std::false_type{}, std::true_type{});
+  // per block: best -K' over the 16 lanes, then the least raster index among its holders
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int key = acc[i];
+    const bool valid = key >= VALID_MIN;
+    const int nk = valid ? key >> 7 : INT_MIN;
+    const int rank = 127 - (key & 127);
+    const int R = r0 + rank / NMT;
+    const int u = 16 * (rank % NMT) + l16;
+    const int j = 4 * (i & 1) + g;
+    const int dy = (i >> 1) ? R - 8 : R;
+    const int ri = dy * N + u - 8 * j;
+    int best = nk;
+    best = max(best, __builtin_amdgcn_update_dpp(INT_MIN, best, 0xB1, 0xf, 0xf, false));
+    best = max(best, __builtin_amdgcn_update_dpp(INT_MIN, best, 0x4E, 0xf, 0xf, false));
+    best = max(best, __builtin_amdgcn_update_dpp(INT_MIN, best, 0x141, 0xf, 0xf, false));
+    best = max(best, __builtin_amdgcn_update_dpp(INT_MIN, best, 0x140, 0xf, 0xf, false));
+    int bri = valid && nk == best ? ri : INT_MAX;
+    bri = min(bri, __builtin_amdgcn_update_dpp(INT_MAX, bri, 0xB1, 0xf, 0xf, false));
+    bri = min(bri, __builtin_amdgcn_update_dpp(INT_MAX, bri, 0x4E, 0xf, 0xf, false));
+    bri = min(bri, __builtin_amdgcn_update_dpp(INT_MAX, bri, 0x141, 0xf, 0xf, false));
+    bri = min(bri, __builtin_amdgcn_update_dpp(INT_MAX, bri, 0x140, 0xf, 0xf, false));
+    if (l16 == 0) {
+      const int blk = 8 * (i >> 1) + j;                  // tile block: row-major, 0..15
+      red[2 * (wave * 16 + blk)] = best;
+      red[2 * (wave * 16 + blk) + 1] = bri;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __restrict__ ref,
+                                                             const uint8_t* __restrict__ cur,
+                                                             int64_t nframes, int H, int W,
+                                                             int64_t* __restrict__ mv) {
+  using namespace mf2;
+  using mf::E_OUT;
+  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_DW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = (int)__builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+  const int g = lane >> 4, l16 = lane & 15;
+  const int h = H / 8, w = W / 8;
+  const int tpr = (w + TBX - 1) / TBX, trows = (h + 1) / 2;
+  const uint32_t tpf = (uint32_t)(trows * tpr);
+  const uint32_t ntiles = (uint32_t)nframes * tpf;
+  const int64_t HW = (int64_t)H * W;
+  struct Loads {
+    uint32_t raw[IPT][3];
+    mf_v4i bop;
+  };
+  auto tile_xy = [&](uint32_t t, uint32_t& f, int& by, int& bx0) {
+    f = t / tpf;
+    const uint32_t rem = t - f * tpf;
+    by = 2 * (int)(rem / (uint32_t)tpr);
+    bx0 = (int)(rem - (uint32_t)(by / 2) * tpr) * TBX;
+  };
+  // lane l16 = 4g' + i (MFMA row) loads quad i's block g': top/bottom i >> 1, column 4 (i & 1) + g'
+  const int qi = l16 & 3, qg = l16 >> 2;
+  auto load = [&](uint32_t t, Loads& L) {
+    const bool exists = t < ntiles;
+    uint32_t f;
+    int by, bx0;
+    tile_xy(exists ? t : 0u, f, by, bx0);
+    const int xb = 8 * bx0 - SR, yb = 8 * by - SR;
+    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(ref + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t*>(cur + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int i = tid + 256 * k;
+      const int row = i / NPAIR, p = i - row * NPAIR;
+      const int y = yb + row;
+      const bool ok = i < ITEMS && y >= 0 && y < H;
+      const int off = ok ? y * W + xb + 8 * p : 0x40000000;
+      const mf_u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
+      L.raw[k][0] = a.x;
+      L.raw[k][1] = a.y;
+      L.raw[k][2] = __builtin_amdgcn_raw_buffer_load_b32(rr, off + 8, 0, 0);
+    }
+    {
+      const int bx = bx0 + 4 * (qi & 1) + qg, byy = by + (qi >> 1);
+      const int off = bx < w && byy < h ? (8 * byy + 2 * g) * W + 8 * bx : 0x40000000;
+      const mf_u32x2 r0 = __builtin_amdgcn_raw_buffer_load_b64(rc, off, 0, 0);
+      const mf_u32x2 r1 = __builtin_amdgcn_raw_buffer_load_b64(rc, off + W, 0, 0);
+      L.bop = mf_v4i{(int)r0.x, (int)r0.y, (int)r1.x, (int)r1.y};
+    }
+  };
+
+  uint32_t tile = blockIdx.x;
+  if ((gridDim.x & 7u) == 0u) tile = (tile & 7u) * (gridDim.x >> 3) + (tile >> 3);   // XCD runs
+  Loads L;
+  load(tile, L);
+  int* red = reinterpret_cast<int*>(lds + RED_OFF);
+  for (; tile < ntiles; tile += gridDim.x) {
+    uint32_t f;
+    int by, bx0;
+    tile_xy(tile, f, by, bx0);
+    __syncthreads();                                   // the previous tile's LDS reads are done
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int i = tid + 256 * k;
+      if (i < ITEMS) {
+        const int row = i / NPAIR, p = i - row * NPAIR;
+        uint32_t* d = lds + row * PITCH + 2 * p;
+        const uint32_t w0 = L.raw[k][0] ^ 0x80808080u, w1 = L.raw[k][1] ^ 0x80808080u,
+                       w2 = L.raw[k][2] ^ 0x80808080u;
+        d[0] = w0;
+        d[1] = w1;
+#pragma unroll
+        for (int s = 1; s < 4; ++s) {
+          d[s * COPY] = __builtin_amdgcn_alignbyte(w1, w0, s);
+          d[s * COPY + 1] = __builtin_amdgcn_alignbyte(w2, w1, s);
+        }
+      }
+    }
+    __syncthreads();
+    {
+      // window energies E[R][u] = B + 128 (-S2') (me_mfma16_kernel's form), two threads per
+      // column u: threads 0..95 the offsets R < 20 from rows 0..26, threads 128..223 the
+      // offsets R >= 20 from rows 20..47 (each a prefix over its rows)
+      const int half = tid >> 7, u = tid & 127;
+      if (u < U) {
+        const uint32_t* cw = lds + (u & 3) * COPY + (u >> 2);
+        const int xb = 8 * bx0 - SR, yb = 8 * by - SR;
+        const bool xok = xb + u >= 0 && xb + u + 8 <= W;
+        const int rlo = half ? 20 : 0, rhi = half ? NR : 20;     // offsets of this thread
+        auto energy = [&](auto hf) {
+          constexpr int RL = decltype(hf)::value ? 20 : 0, RH = decltype(hf)::value ? NR : 20;
+          int P[RH + 7 - RL + 1];
+          int pr = 0;
+#pragma unroll
+          for (int r = RL; r < RH + 7; ++r) {
+            const int w0 = (int)cw[r * PITCH], w1 = (int)cw[r * PITCH + 1];
+            pr = __builtin_amdgcn_sdot4(w1, w1, __builtin_amdgcn_sdot4(w0, w0, pr, false), false);
+            P[r - RL] = pr;
+            if (r >= RL + 7) {
+              const int R = r - 7;
+              const int t = (r - 8 >= RL ? P[r - 8 - RL] : 0) - pr;
+              const int wv = R < 11 ? 0 : (R - 1) / 10;
+              const int rank = (R - wave_r0(wv)) * NMT + (u >> 4);
+              const bool ok = xok && (unsigned)(yb + R) <= (unsigned)(H - 8);
+              lds[E_OFF + R * U + u] = (uint32_t)((ok ? (1 << 27) + 127 - rank : E_OUT) + 128 * t);
+            }
+          }
+        };
+        (void)rlo;
+        (void)rhi;
+        if (half) energy(std::true_type{});
+        else energy(std::false_type{});
+      }
+    }
+    const mf_v4i bop = mf_v4i{L.bop.x ^ (int)0x80808080u, L.bop.y ^ (int)0x80808080u,
+                              L.bop.z ^ (int)0x80808080u, L.bop.w ^ (int)0x80808080u};
+    __syncthreads();
+    load(tile + gridDim.x, L);                          // the next tile's inputs, in flight
+    if (wave == 0) me2_search<0>(lds, red, wave, g, l16, bop);
+    else if (wave == 3) me2_search<3>(lds, red, wave, g, l16, bop);
+    else me2_search<1>(lds, red, wave, g, l16, bop);
+    __syncthreads();
+    if (tid < 16) {
+      const int blk = tid, bx = bx0 + (blk & 7), byy = by + (blk >> 3);
+      int k = red[2 * blk], ri = red[2 * blk + 1];
+#pragma unroll
+      for (int ww = 1; ww < 4; ++ww) {
+        const int ok_ = red[2 * (ww * 16 + blk)], oi = red[2 * (ww * 16 + blk) + 1];
+        if (ok_ > k || (ok_ == k && oi < ri)) {
+          k = ok_;
+          ri = oi;
+        }
+      }
+      if (bx < w && byy < h)
+        mv[((int64_t)f * h + byy) * w + bx] = ri == INT_MAX ? (int64_t)SR * N + SR : (int64_t)ri;
+    }
+  }
+}
+
 // One chunk of frame pairs on the matrix cores.  Returns false when the kernel does not apply
 // (the caller keeps its own path): a frame of 2 GiB or more, or 2^31 tiles.
 bool launch_me_mfma16(const uint8_t* ref, const uint8_t* cur, int64_t nf, int H, int W, int64_t* mv,
                       hipStream_t s) {
   if ((int64_t)H * W >= ((int64_t)1 << 31)) return false;
   const int h = H / 8, w = W / 8;
+  if (IVC_ME_2ROW) {
+    const int64_t tiles2 = nf * ((h + 1) / 2) * ((w + mf2::TBX - 1) / mf2::TBX);
+    if (tiles2 <= 0) return true;
+    if (tiles2 >= ((int64_t)1 << 31)) return false;
+    int64_t grid = 2 * (int64_t)resident_grid_ptr(reinterpret_cast<const void*>(me_mfma16x2_kernel), tiles2);
+    if (grid > tiles2) grid = tiles2;
+    me_mfma16x2_kernel<<<(unsigned)grid, 256, 0, s>>>(ref, cur, nf, H, W, mv);
+    return true;
+  }
   const int64_t tiles = nf * h * ((w + mf::TB - 1) / mf::TB);
   if (tiles <= 0) return true;
   if (tiles >= ((int64_t)1 << 31)) return false;     // 32-bit tile counters
