@@ -1124,6 +1124,11 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # start the ranks ourselves (nothing has touched the GPU yet) and pass their status on
         sys.exit(subprocess.call(launcher_cmd(args.gpus, sys.argv[1:], free_port())))
+    # stdout carries exactly the one JSON line: libraries that print to file descriptor 1
+    # (RCCL's version banner at communicator creation) write to stderr instead
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     dist, rank, world, local = dist_setup(args.gpus, rccl_world1=args.rccl)
     dev = torch.device("cuda", torch.cuda.current_device())
     from ivclab_amd import PatchQuant
@@ -1218,7 +1223,7 @@ def main():
                             "checked_rank0": verify["checked"]}
     result["bench_wall_s"] = round(time.perf_counter() - t_start, 1)
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        os.write(json_fd, (json.dumps(result) + "\n").encode())
     if dist is not None or FORCE_COLL:
         import torch.distributed as tdist
         tdist.destroy_process_group()

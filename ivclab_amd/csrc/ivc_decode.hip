@@ -22,6 +22,7 @@
 //               time (2 x nb x 192 contiguous bytes) through a 3 KB staging area.
 // HBM per block: C x 256 B in, 1536 B out.  Stores are non-temporal (streamed output).
 #include <algorithm>
+#include <type_traits>
 
 #include "ivc_internal.h"
 #include "ivc_math.h"
@@ -48,6 +49,15 @@ constexpr int DQ_PITCH = 68;     // int32 per staged block-plane (16-byte rows, 
 constexpr int DX_WAVE = 8 * 72;  // doubles per wave: transpose image [b][k pitch 9] / staging
 #ifndef IVC_DEC_STORE_AUX
 #define IVC_DEC_STORE_AUX 2      // nt: streamed output
+#endif
+// (A/B) the parse with 4 symbols per lane
+#ifndef IVC_DEC_PARSE4
+#define IVC_DEC_PARSE4 1
+#endif
+// ablation builds only (tools/ab), bits: 1 = the image stores skipped (behind a runtime test the
+// compiler cannot fold), 2 = sym_image_kernel's parse skipped (the staging stays zero)
+#ifndef IVC_DEC_ABLATE
+#define IVC_DEC_ABLATE 0
 #endif
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t dec_rsrc(const void* base, uint32_t bytes) {
@@ -100,10 +110,12 @@ __device__ __forceinline__ void dec_load(const DecArgs& a, int64_t g, int lane, 
 // qs + (b * C + p) * DQ_PITCH, zig-zag or raster order inside) and its output: DEC_BLOCKS
 // [nblk][3][8][8] or DEC_IMAGE rows.  Shared by intra_decode_kernel (coefficients from HBM) and
 // sym_image_kernel (coefficients expanded from the zero-run stream).
-// FASTDQ: |q * table| < 2^31 is known (int16 coefficients, finite |table| < 2^16, checked on
+// DQ_FAST: |q * table| < 2^31 is known (int16 coefficients, finite |table| < 2^16, checked on
 // the host), so NumPy's float64 -> int32 cast of the dequantised value is a truncation
-// (v_trunc_f64) with no range handling.
-template <int C, int OUTL, bool RGB, typename Q = int32_t, int QP = DQ_PITCH, bool FASTDQ = false>
+// (v_trunc_f64) with no range handling.  DQ_INT: every table entry is moreover a positive
+// integer, so q * table is an exact integer (no truncation) and never -0.0.
+enum { DQ_GENERAL = 0, DQ_FAST = 1, DQ_INT = 2 };
+template <int C, int OUTL, bool RGB, typename Q = int32_t, int QP = DQ_PITCH, int DQM = DQ_GENERAL>
 __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup& G,
                                                const Q* qs, double* xs, const double* tq,
                                                const uint32_t* pos, int b, int r, int lane) {
@@ -119,19 +131,26 @@ __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup&
     double x[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {  // patchquant.py:77-78: int32 * table (float64), truncated
-      if constexpr (FASTDQ)   // + 0.0: a truncated -0.x is -0.0, the int32 round trip gives +0.0
+      if constexpr (DQM == DQ_INT)
+        x[k] = (double)qv[k] * tq[p * 64 + r * 8 + k];
+      else if constexpr (DQM == DQ_FAST)   // + 0.0: a truncated -0.x is -0.0, the int32 round trip gives +0.0
         x[k] = __builtin_trunc((double)qv[k] * tq[p * 64 + r * 8 + k]) + 0.0;
       else
         x[k] = (double)np_to_i32<double>((double)qv[k] * tq[p * 64 + r * 8 + k]);
     }
-    dct3_line<double>(x, 0.25, true);                 // axis -1 (row r)
+    // both passes' ortho factor 1/4 applied once at the end as 1/16: every step is a sum,
+    // difference or product with a constant, exact under power-of-two scaling (the values
+    // are far from the subnormal and overflow ranges), so the result is bit-identical
+    dct3_line<double>(x, 1.0, true);                  // axis -1 (row r)
 #pragma unroll
     for (int k = 0; k < 8; ++k) xs[b * 72 + r * 9 + k] = x[k];
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = xs[b * 72 + i * 9 + r];
     __builtin_amdgcn_wave_barrier();
-    dct3_line<double>(x, 0.25, true);                 // axis -2 (column r)
+    dct3_line<double>(x, 1.0, true);                  // axis -2 (column r)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = x[i] * 0.0625;
     if constexpr (OUTL == DEC_BLOCKS) {
       // plane p of the group's blocks: [b][i][r], 8 x 512 B, block b's plane at
       // out + ((blk0 + b) * 3 + p) * 64
@@ -171,10 +190,10 @@ __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup&
         }
       }
     }
-    // two image rows at a time: stage [ri][px = 8 b + r][p], then 16-byte stores of the
-    // rows' nb * 192 contiguous bytes each
     const int nb12 = G.nb * 12;
     double* rowp = a.out + (G.row * 8) * a.W3 + (int64_t)G.bx0 * 24;
+    // two image rows at a time: stage [ri][px = 8 b + r][p], then 16-byte stores of the
+    // rows' nb * 192 contiguous bytes each
 #pragma unroll
     for (int i0 = 0; i0 < 8; i0 += 2) {
 #pragma unroll
@@ -189,8 +208,9 @@ __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup&
         for (int j = 0; j < 2; ++j) {
           const int c = j * 64 + lane;                // chunk of this row (96 at most)
           const dec_u32x4 v = *reinterpret_cast<const dec_u32x4*>(xs + ri * 192 + c * 2);
-          __builtin_amdgcn_raw_buffer_store_b128(v, ro, c < 96 ? c * 16 : 0x40000000, 0,
-                                                 IVC_DEC_STORE_AUX);
+          if (!(IVC_DEC_ABLATE & 1) || a.W3 < 0)
+            __builtin_amdgcn_raw_buffer_store_b128(v, ro, c < 96 ? c * 16 : 0x40000000, 0,
+                                                   IVC_DEC_STORE_AUX);
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -289,7 +309,7 @@ constexpr int SYM_QP = 72;                             // int16 per staged block
 constexpr int SYM_XW = SYM_SEG + 8;                    // int32 words: [3] = prev, [4 ..] symbols
 constexpr int SYM_XD = (SYM_XW / 2 > DX_WAVE ? SYM_XW / 2 : DX_WAVE);   // doubles per wave
 
-template <int C, bool RGB, bool FASTDQ>
+template <int C, bool RGB, int DQM>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t) {
   constexpr int QS = 8 * C * SYM_QP;                   // int16 per wave
   __shared__ __attribute__((aligned(16))) int16_t qs_all[4 * QS];
@@ -337,7 +357,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
     int pcarry = 0;         // coefficients of the group before the chunk
     int bpcarry = 0;        // EOBs before the chunk
     int prevc = 1;          // the symbol before the round (a group starts at a value slot)
-    for (int s0 = 0; s0 < len; s0 += SYM_SEG) {
+    if (IVC_DEC_ABLATE & 2) bpcarry = nbp;
+    for (int s0 = 0; s0 < ((IVC_DEC_ABLATE & 2) ? 0 : len); s0 += SYM_SEG) {
       // one round: every load in flight, then the LDS writes
       dec_u32x4 v[SYM_SEG / 256];
 #pragma unroll
@@ -354,6 +375,60 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
       }
       __builtin_amdgcn_wave_barrier();
       const int rlen = len - s0 < SYM_SEG ? len - s0 : SYM_SEG;
+#if IVC_DEC_PARSE4
+      // 4 symbols per lane (lane l: symbols 4l .. 4l + 3 of a 256-symbol chunk): one wave scan
+      // and one LDS round trip per 256 symbols.  A run length is clamped to 127 (anything past
+      // 64 already makes its block-plane fail the offset checks), so a chunk's coefficient
+      // count fits 16 bits and the EOB count sits above it.
+      for (int c0 = 0; c0 < rlen; c0 += 256) {
+        const int i0 = c0 + 4 * lane;
+        const dec_u32x4 q = *reinterpret_cast<const dec_u32x4*>(st + i0);
+        const int pvs = st[i0 - 1], nxs = st[i0 + 4];
+        const int v[4] = {(int)q.x, (int)q.y, (int)q.z, (int)q.w};
+        int pk[4];
+        bool eobf[4], isval[4];
+        int lt = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int prv = e ? v[e - 1] : pvs, nx = e < 3 ? v[e + 1] : nxs;
+          const bool valid = i0 + e < rlen;
+          const bool rl = prv == 0;                    // a run-length slot
+          eobf[e] = valid && !rl && v[e] == z.eob;
+          isval[e] = valid && !rl && !eobf[e];
+          const int run = nx < 1 ? 1 : (nx > 127 ? 127 : nx);
+          const int cc = isval[e] ? (v[e] == 0 ? run : 1) : 0;
+          pk[e] = (eobf[e] ? (1 << 16) : 0) | cc;
+          lt += pk[e];
+        }
+        const int incl = dec_wave_incl_sum(lt);
+        int pre = incl - lt;
+        int pex[4], bp[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          pex[e] = pcarry + (pre & 0xffff);          // this slot's coefficient offset
+          bp[e] = bpcarry + (pre >> 16);              // its block-plane
+          pre += pk[e];
+          if (eobf[e] && bp[e] < nbp) bps[bp[e] + 1] = pex[e];
+        }
+        __builtin_amdgcn_wave_barrier();
+        // every block-plane start read first (one LDS wait), then the checks and the writes
+        int bs[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bs[e] = bps[bp[e] < nbp ? bp[e] : 0];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool bpok = bp[e] < nbp;
+          const int off = pex[e] - bs[e];             // offset inside the block-plane
+          const bool nzv = isval[e] && v[e] != 0;
+          const bool wr = nzv && off < 64 && bpok && v[e] == (int)(int16_t)v[e];
+          bad |= (nzv && !wr) || (eobf[e] && (off > 64 || !bpok));
+          if (wr) qs[__umul24(bp[e], SYM_QP) + off] = (int16_t)v[e];
+        }
+        const int tot = __builtin_amdgcn_readlane(incl, 63);
+        pcarry += tot & 0xffff;
+        bpcarry += tot >> 16;
+      }
+#else
       for (int c0 = 0; c0 < rlen; c0 += 64) {
         const int i = c0 + lane;
         const int cur = st[i], prv = st[i - 1], nx = st[i + 1];
@@ -383,11 +458,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
         pcarry += tot & 0xfffff;
         bpcarry += tot >> 20;
       }
+#endif
       prevc = st[SYM_SEG - 1];
     }
     if (bpcarry != nbp) bad = true;
     __builtin_amdgcn_wave_barrier();
-    dec_group_math<C, DEC_IMAGE, RGB, int16_t, SYM_QP, FASTDQ>(a, G, qs, xs, tq, pos, b, r, lane);
+    dec_group_math<C, DEC_IMAGE, RGB, int16_t, SYM_QP, DQM>(a, G, qs, xs, tq, pos, b, r, lane);
   }
   if (__ballot(bad) && lane == 0) atomicOr(z.fail, 1);
 }
@@ -511,17 +587,29 @@ hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const ui
     const unsigned grid = resident_grid_ptr(reinterpret_cast<const void*>(k), (a.ngroups + 3) / 4);
     k<<<grid, 256, 0, s>>>(a, z, t);
   };
-  // int16 coefficients times a finite table below 2^16 in magnitude stay inside int32
-  bool fast = true;
-  for (int i = 0; i < 192; ++i)
-    if (!(__builtin_fabs(t.q[i]) < 65536.0)) fast = false;
-  if (C == 3) {
-    if (to_rgb) { if (fast) go(sym_image_kernel<3, true, true>); else go(sym_image_kernel<3, true, false>); }
-    else { if (fast) go(sym_image_kernel<3, false, true>); else go(sym_image_kernel<3, false, false>); }
-  } else {
-    if (to_rgb) { if (fast) go(sym_image_kernel<1, true, true>); else go(sym_image_kernel<1, true, false>); }
-    else { if (fast) go(sym_image_kernel<1, false, true>); else go(sym_image_kernel<1, false, false>); }
+  // int16 coefficients times a finite table below 2^16 in magnitude stay inside int32 (and
+  // with a table of positive integers the product is exact)
+  bool fast = true, integral = true;
+  for (int i = 0; i < 192; ++i) {
+    const double v = t.q[i];
+    if (!(__builtin_fabs(v) < 65536.0)) fast = false;
+    if (!(v > 0.0 && v < 65536.0 && v == __builtin_trunc(v))) integral = false;
   }
+  const int dqm = !fast ? DQ_GENERAL : (integral ? DQ_INT : DQ_FAST);
+  auto pick = [&](auto rgb_c) {
+    constexpr bool R = decltype(rgb_c)::value;
+    if (C == 3) {
+      if (dqm == DQ_INT) go(sym_image_kernel<3, R, DQ_INT>);
+      else if (dqm == DQ_FAST) go(sym_image_kernel<3, R, DQ_FAST>);
+      else go(sym_image_kernel<3, R, DQ_GENERAL>);
+    } else {
+      if (dqm == DQ_INT) go(sym_image_kernel<1, R, DQ_INT>);
+      else if (dqm == DQ_FAST) go(sym_image_kernel<1, R, DQ_FAST>);
+      else go(sym_image_kernel<1, R, DQ_GENERAL>);
+    }
+  };
+  if (to_rgb) pick(std::true_type{});
+  else pick(std::false_type{});
   return hipGetLastError();
 }
 

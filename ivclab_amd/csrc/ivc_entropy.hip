@@ -400,8 +400,10 @@ constexpr int ZW_STAGE_D = ZW_STAGE + 4 + 68;   // dummy words: 64 lanes + 1, pa
 __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict__ src, int64_t nblk,
                                                       int32_t eob, const int64_t* __restrict__ goff,
                                                       int64_t* __restrict__ off,
-                                                      int32_t* __restrict__ out, int64_t capacity) {
+                                                      int32_t* __restrict__ out, int64_t capacity,
+                                                      const int32_t* run_if) {
   __shared__ __attribute__((aligned(16))) int32_t stage[4 * ZW_STAGE_D];
+  if (run_if && *run_if == 0) return;           // (the int8 hand-off path emitted instead)
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -490,6 +492,193 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
   }
 }
 
+// ---- dense rows through an int8 hand-off (r04) -------------------------------------------
+// The two passes above read the 256-byte rows twice (count, emit).  Here the count pass
+// (zc_count_kernel: one wave per group of ZC_BLK = 16 blocks, lane k = coefficient k, so a
+// block's nonzero mask is one ballot and its count scalar bit operations) also stores the
+// group's coefficients as int8 — lane k's 16 bytes = coefficient k of the 16 blocks — or, for
+// a group with a value outside int8, as int16 in a slot of a small side area.  The emission
+// pass (zc_emit_kernel) reads 1 KB per group instead of 4 KB and places every block's symbols
+// with ballot/mbcnt into the wave's LDS window, then stores the group's contiguous range.
+// A value outside int16 (or the int16 slots running out) sets `bad`: the emitter stands down
+// and zw_emit_kernel runs from the int32 rows instead (gated on the device).
+#ifndef IVC_ZC
+#define IVC_ZC 0
+#endif
+constexpr int ZC_BLK = 16;
+constexpr int ZC_WIN = 1664;   // words per wave: the group's <= 16 x 97 symbols + 65 dummy words
+
+struct ZcScratch {
+  uint8_t* c8;       // [ng][64 lanes][16 B]
+  uint8_t* c16;      // [cap16][64 lanes][32 B]
+  int32_t* flag;     // [ng]: 0, or the group's int16 slot + 1
+  int32_t* ctl;      // [0] int16 slots taken, [1] bad
+  int64_t cap16;
+};
+
+__global__ __launch_bounds__(256) void zc_count_kernel(const int32_t* __restrict__ src, int64_t nblk,
+                                                       int32_t* __restrict__ gcounts, ZcScratch z) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t ng = (nblk + ZC_BLK - 1) / ZC_BLK;
+  // the next group's rows are loaded while this group is counted and packed
+  auto load = [&](int64_t g, int32_t (&x)[ZC_BLK]) {
+    const int64_t b0 = g * ZC_BLK;
+    const int nb = (int)(nblk - b0 < ZC_BLK ? nblk - b0 : ZC_BLK);
+#pragma unroll
+    for (int b = 0; b < ZC_BLK; ++b)
+      x[b] = b < nb ? __builtin_nontemporal_load(src + (b0 + b) * 64 + lane) : 0;
+  };
+  int32_t cur[ZC_BLK];
+  if (wave < ng) load(wave, cur);
+  for (int64_t g = wave; g < ng; g += nw) {
+    int32_t nxt[ZC_BLK];
+    if (g + nw < ng) load(g + nw, nxt);
+    const int nb = (int)(nblk - g * ZC_BLK < ZC_BLK ? nblk - g * ZC_BLK : ZC_BLK);
+    int total = 0;
+    bool wide = false, wider = false;
+#pragma unroll
+    for (int b = 0; b < ZC_BLK; ++b) {
+      const uint64_t m = __ballot(cur[b] != 0);
+      const int lz = m ? __builtin_clzll(m) : 64;
+      const uint64_t inside = m ? ~0ull >> lz : 0ull;       // bits [0, last nonzero]
+      const uint64_t zeros = ~m & inside;
+      const uint64_t st = zeros & ~(zeros << 1);            // run starts
+      total += b < nb ? __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1 : 0;
+      wide |= (uint32_t)(cur[b] + 128) > 255u;
+      wider |= (uint32_t)(cur[b] + 32768) > 65535u;
+    }
+    if (lane == 0) gcounts[g] = total;
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    uint32_t w8[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      w8[k] = ((uint32_t)cur[4 * k] & 0xffu) | ((uint32_t)cur[4 * k + 1] & 0xffu) << 8 |
+              ((uint32_t)cur[4 * k + 2] & 0xffu) << 16 | ((uint32_t)cur[4 * k + 3] & 0xffu) << 24;
+    *reinterpret_cast<u32x4*>(z.c8 + (g * 64 + lane) * 16) = u32x4{w8[0], w8[1], w8[2], w8[3]};
+    int flag = 0;
+    if (__ballot(wide)) {                                     // wave-uniform, rare
+      if (__ballot(wider)) {
+        if (lane == 0) atomicOr(z.ctl + 1, 1);
+      } else {
+        int slot = 0;
+        if (lane == 0) slot = atomicAdd(z.ctl, 1);
+        slot = __shfl(slot, 0);
+        if (slot < z.cap16) {
+          uint32_t w16[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k)
+            w16[k] = ((uint32_t)cur[2 * k] & 0xffffu) | ((uint32_t)cur[2 * k + 1] & 0xffffu) << 16;
+          u32x4* d16 = reinterpret_cast<u32x4*>(z.c16 + ((int64_t)slot * 64 + lane) * 32);
+          d16[0] = u32x4{w16[0], w16[1], w16[2], w16[3]};
+          d16[1] = u32x4{w16[4], w16[5], w16[6], w16[7]};
+          flag = slot + 1;
+        } else if (lane == 0) {
+          atomicOr(z.ctl + 1, 1);
+        }
+      }
+    }
+    if (lane == 0) z.flag[g] = flag;
+#pragma unroll
+    for (int b = 0; b < ZC_BLK; ++b) cur[b] = nxt[b];
+  }
+}
+
+// one wave per group; the block offsets off[blk] are written here (the scan wrote the group
+// offsets and the stream length)
+__global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
+                                                      const int64_t* __restrict__ goff,
+                                                      const uint8_t* __restrict__ c8,
+                                                      const uint8_t* __restrict__ c16,
+                                                      const int32_t* __restrict__ gflag,
+                                                      const int32_t* __restrict__ bad,
+                                                      int64_t* __restrict__ off,
+                                                      int32_t* __restrict__ out, int64_t capacity) {
+  __shared__ __attribute__((aligned(16))) int32_t win[4 * ZC_WIN];
+  if (*bad) return;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t ng = (nblk + ZC_BLK - 1) / ZC_BLK;
+  int32_t* const os = win + wave * ZC_WIN;
+  int32_t* const dummy = os + ZC_WIN - 65 + lane;
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  struct Pre {
+    int64_t base;
+    int flag;
+    i32x4 w;
+  };
+  auto fetch = [&](int64_t g, Pre& P) {
+    P.base = goff[g];
+    P.flag = gflag[g];
+    P.w = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(c8 + (g * 64 + lane) * 16));
+  };
+  const int64_t g0 = (int64_t)blockIdx.x * 4 + wave;
+  Pre cur;
+  if (g0 < ng) fetch(g0, cur);
+  for (int64_t g = g0; g < ng; g += nw) {
+    Pre nxt;
+    if (g + nw < ng) fetch(g + nw, nxt);
+    const int nb = (int)(nblk - g * ZC_BLK < ZC_BLK ? nblk - g * ZC_BLK : ZC_BLK);
+    int32_t xv[ZC_BLK];
+    if (cur.flag == 0) {
+#pragma unroll
+      for (int e = 0; e < ZC_BLK; ++e)
+        xv[e] = (int32_t)(int8_t)(uint8_t)((uint32_t)cur.w[e / 4] >> (8 * (e & 3)));
+    } else {                                                  // rare: the group's int16 slot
+      const i32x4* src = reinterpret_cast<const i32x4*>(c16 + ((int64_t)(cur.flag - 1) * 64 + lane) * 32);
+      const i32x4 a0 = src[0], a1 = src[1];
+#pragma unroll
+      for (int e = 0; e < ZC_BLK; ++e) {
+        const uint32_t word = (uint32_t)(e < 8 ? a0[e / 2] : a1[(e - 8) / 2]);
+        xv[e] = (int32_t)(int16_t)(uint16_t)(word >> (16 * (e & 1)));
+      }
+    }
+    int fill = 0, offv = 0;
+#pragma unroll
+    for (int b = 0; b < ZC_BLK; ++b) {
+      if (b < nb) {                                           // wave-uniform
+      // same slots and values as zr_group_emit_fit (ivc_kernels.hip): a nonzero, a run's 0 and
+      // its length, or the EOB on the first zero after the last nonzero
+      const int32_t x = xv[b];
+      const bool nz = x != 0;
+      const uint64_t m = __ballot(nz);
+      const uint64_t later = m >> lane;
+      const bool hl = later != 0;
+      const uint64_t pm = (m << 1) | 1ull, hm = __ballot(hl);
+      const uint64_t st = pm & hm & ~m;
+      const bool pnz = __builtin_amdgcn_inverse_ballot_w64(pm);
+      const bool rs = __builtin_amdgcn_inverse_ballot_w64(st);
+      const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
+      const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
+                      2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
+      const bool w1 = nz || pnz;
+      const int32_t v1 = nz || hl ? x : eob;
+      const int32_t v2 = rs ? (int32_t)__builtin_ctzll(later) : eob;
+      int32_t* const d = w1 ? os + fill + pos : dummy;
+      d[1] = v2;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // keep the two writes ordered
+      d[0] = v1;
+      offv = lane == b ? fill : offv;
+      fill += cnt;
+      }
+    }
+    if (lane < nb) off[g * ZC_BLK + lane] = cur.base + offv;
+    __builtin_amdgcn_wave_barrier();
+    // the group's symbols are the contiguous range [base, base + fill); stored while they fit
+    // the caller's capacity (the buffer range drops the rest)
+    const int64_t lim = capacity - cur.base;
+    const int nst = (int)(lim < (int64_t)fill ? (lim > 0 ? lim : 0) : (int64_t)fill);
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
+        out + (nst > 0 ? cur.base : 0), 0, 4 * nst, 0x00020000);
+    for (int j0 = 0; j0 < fill; j0 += 64)
+      __builtin_amdgcn_raw_buffer_store_b32(os[j0 + lane], ro, 4 * (j0 + lane), 0, 0);
+    __builtin_amdgcn_wave_barrier();
+    cur = nxt;
+  }
+}
+
 static bool zw_ok(const int32_t* src, int stride, int B) {
   return stride == 64 && B == 64 && ((uintptr_t)src & 15u) == 0;
 }
@@ -518,11 +707,21 @@ struct GroupOffsetSink {
 // Scratch of launch_zerorun_offsets / launch_zerorun_emit: per-block int32 counts (generic
 // path) or per-group int32 counts + int64 group offsets (wide path), and the scan's
 // aggregates.
-int64_t zerorun_scratch_bytes(int64_t nblk) {
+// + the int8 hand-off (zc_*): c8, per-group flags, 2 control words, int16 slots for 1 in 8
+// groups (more wide groups send the call to zw_emit_kernel)
+static int64_t zc_cap16(int64_t ng) { return ng / 8 + 64; }
+static int64_t zr_base_bytes(int64_t nblk) {
   const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
   const int64_t wide = ((4 * ng + 7) & ~int64_t(7)) + 8 * (ng + 1);
   const int64_t cnt = 4 * nblk > wide ? 4 * nblk : wide;
-  return ((cnt + 7) & ~int64_t(7)) + 8 * scan_scratch_elems(nblk);
+  return ((((cnt + 7) & ~int64_t(7)) + 8 * scan_scratch_elems(nblk)) + 255) & ~int64_t(255);
+}
+static int64_t zc_bytes(int64_t nblk) {
+  const int64_t ng = (nblk + ZC_BLK - 1) / ZC_BLK;
+  return 1024 * ng + ((4 * ng + 255) & ~int64_t(255)) + 256 + 2048 * zc_cap16(ng);
+}
+int64_t zerorun_scratch_bytes(int64_t nblk) {
+  return zr_base_bytes(nblk) + (IVC_ZC ? zc_bytes(nblk) : 0);
 }
 
 namespace {
@@ -530,6 +729,7 @@ struct ZrScratch {
   int32_t* counts;   // per block (generic) or per group (wide)
   int64_t* goff;     // wide path: ng + 1 group offsets
   int64_t* agg;
+  ZcScratch zc;
 };
 ZrScratch zr_scratch(void* scratch, int64_t nblk) {
   const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
@@ -540,6 +740,15 @@ ZrScratch zr_scratch(void* scratch, int64_t nblk) {
   z.counts = (int32_t*)b;
   z.goff = (int64_t*)(b + ((4 * ng + 7) & ~int64_t(7)));
   z.agg = (int64_t*)(b + ((cnt + 7) & ~int64_t(7)));
+  char* c = b + zr_base_bytes(nblk);
+  z.zc.c8 = (uint8_t*)c;
+  c += 1024 * ng;
+  z.zc.flag = (int32_t*)c;
+  c += (4 * ng + 255) & ~int64_t(255);
+  z.zc.ctl = (int32_t*)c;
+  c += 256;
+  z.zc.c16 = (uint8_t*)c;
+  z.zc.cap16 = zc_cap16(ng);
   return z;
 }
 }  // namespace
@@ -552,7 +761,13 @@ hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, 
   const ZrScratch z = zr_scratch(scratch, nblk);
   if (zw_ok(src, stride, B)) {
     const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
-    zw_count_kernel<<<zw_grid((nblk + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(src, nblk, z.counts);
+    if (IVC_ZC) {
+      hipError_t e = hipMemsetAsync(z.zc.ctl, 0, 8, s);
+      if (e != hipSuccess) return e;
+      zc_count_kernel<<<zw_grid(nblk, 8), 256, 0, s>>>(src, nblk, z.counts, z.zc);
+    } else {
+      zw_count_kernel<<<zw_grid((nblk + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(src, nblk, z.counts);
+    }
     return device_scan<int64_t>(ng, CountGen{z.counts}, SumI64{}, GroupOffsetSink{z.goff, ng, off + nblk},
                                 z.agg, s);
   }
@@ -576,8 +791,11 @@ hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int
   if (nblk <= 0) return hipSuccess;
   if (zw_ok(src, stride, B)) {
     const ZrScratch z = zr_scratch(scratch, nblk);
+    if (IVC_ZC)
+      zc_emit_kernel<<<zw_grid(nblk, 6), 256, 0, s>>>(nblk, eob, z.goff, z.zc.c8, z.zc.c16, z.zc.flag,
+                                                      z.zc.ctl + 1, off, out, capacity);
     zw_emit_kernel<<<zw_grid((nblk + IVC_ZW_EMIT_GROUPS - 1) / IVC_ZW_EMIT_GROUPS, 6), 256, 0, s>>>(
-        src, nblk, eob, z.goff, off, out, capacity);
+        src, nblk, eob, z.goff, off, out, capacity, IVC_ZC ? z.zc.ctl + 1 : nullptr);
   } else {
     zr_emit_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, eob, off, out, capacity);
   }
@@ -720,33 +938,49 @@ constexpr int ZF_TILE = 4096, ZF_HALO = 128;
 
 // (eobmask, optional: bit i of word t * 128 + i / 32 = symbol t * ZF_TILE + i is an EOB slot —
 // the symbols -> image path locates its groups from it)
+// The next tile's loads are issued before this tile is counted (a wave has 8 KB of reads in
+// flight instead of 4: one load latency per tile measured 3.3 ms for the cfg3 stream, 4.3 TB/s).
+struct ZfTile {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  i32x4 q[ZF_TILE / 1024];
+  int p0[ZF_TILE / 1024];
+};
+__device__ __forceinline__ void zf_load_tile(const int32_t* __restrict__ s, int64_t n, int64_t t,
+                                             int tid, ZfTile& T) {
+#pragma unroll
+  for (int k = 0; k < ZF_TILE / 1024; ++k) {
+    const int64_t i = t * ZF_TILE + (int64_t)(k * 256 + tid) * 4;
+    if (i + 3 < n) {
+      T.q[k] = __builtin_nontemporal_load(reinterpret_cast<const ZfTile::i32x4*>(s + i));
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) T.q[k][e] = i + e < n ? s[i + e] : 1;
+    }
+    // the symbol before the wave's first: one scalar load per wave (a wave-uniform address),
+    // issued with the quads — not a per-lane load (one dword load per lane doubled the vector
+    // memory instructions), nor a lane-0 vector load after the quad (a second latency)
+    const int64_t iw = (int64_t)__builtin_amdgcn_readfirstlane((int)(i - t * ZF_TILE)) + t * ZF_TILE;
+    T.p0[k] = iw > 0 && iw <= n ? s[iw - 1] : 1;   // the stream's first slot is a value slot
+  }
+}
 __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict__ s, int64_t n,
                                                        int32_t eob, int32_t* __restrict__ tile_eobs,
                                                        int* fail, uint32_t* __restrict__ eobmask) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int64_t ntiles = (n + ZF_TILE - 1) / ZF_TILE;
+  ZfTile cur;
+  if ((int64_t)blockIdx.x < ntiles) zf_load_tile(s, n, blockIdx.x, tid, cur);
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    ZfTile nxt;
+    if (t + gridDim.x < ntiles) zf_load_tile(s, n, t + gridDim.x, tid, nxt);
     int cnt = 0;
     bool bad = false;
 #pragma unroll
     for (int k = 0; k < ZF_TILE / 1024; ++k) {
       const int64_t i = t * ZF_TILE + (int64_t)(k * 256 + tid) * 4;
-      int v[4];
-      if (i + 3 < n) {
-        typedef int i32x4 __attribute__((ext_vector_type(4)));
-        const i32x4 q = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(s + i));
-        v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = i + e < n ? s[i + e] : 1;
-      }
-      // the symbol before: the previous lane's last (DPP); lane 0's comes from one scalar load
-      // per wave (a wave-uniform address), issued with the quads — not a per-lane load (one
-      // dword load per lane doubled the vector memory instructions), nor a lane-0 vector load
-      // after the quad (a second latency: 3.79 vs 3.46 ms)
-      const int64_t iw = (int64_t)__builtin_amdgcn_readfirstlane((int)(i - t * ZF_TILE)) + t * ZF_TILE;
-      const int p0 = iw > 0 && iw <= n ? s[iw - 1] : 1;   // the stream's first slot is a value slot
-      int pv = __builtin_amdgcn_update_dpp(p0, v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
+      const int v[4] = {cur.q[k].x, cur.q[k].y, cur.q[k].z, cur.q[k].w};
+      // the symbol before: the previous lane's last (DPP), lane 0's from the scalar load
+      int pv = __builtin_amdgcn_update_dpp(cur.p0[k], v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
       uint32_t bits = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -771,6 +1005,7 @@ __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict
     for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
     if (__ballot(bad) && lane == 0) atomicOr(fail, 1);
     if (lane == 0 && cnt) atomicAdd(tile_eobs + t, cnt);    // tile_eobs zeroed by the caller
+    cur = nxt;
   }
 }
 

@@ -920,6 +920,9 @@ __device__ __forceinline__ uint32_t zh_bin(const FusedArgs& a, int32_t v, int la
 // m >> lane != 0), their ballot feeds the lane's slot (two mbcnt) — so the scalar unit keeps
 // only the two popcounts and the running fill per block-plane, and no block has a window
 // check (one basic block for the group).  Same slots and values as the general path below.
+#ifndef IVC_EMIT_FLUSH4
+#define IVC_EMIT_FLUSH4 0
+#endif
 template <int C, bool DUP, bool HIST>
 __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* os, int64_t gbase,
                                                   int gcount, const int32_t (&xv)[8][(C == 1 && DUP) ? 2 : 3],
@@ -977,6 +980,32 @@ __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* o
   const int nst = (int)(lim < (int64_t)fill ? (lim > 0 ? lim : 0) : (int64_t)fill);
   const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
       a.zr_out + (nst > 0 ? gbase : 0), 0, 4 * nst, 0x00020000);
+#if IVC_EMIT_FLUSH4
+  // 4 symbols per lane: 16-byte LDS reads and stores of whole quads (a quad reaching past the
+  // stored range goes word by word: the buffer range check is not per word)
+  typedef int fq_i32x4 __attribute__((ext_vector_type(4)));
+  for (int j0 = 0; j0 < fill; j0 += 256) {
+    const int j = j0 + 4 * lane;
+    const fq_i32x4 v = *reinterpret_cast<const fq_i32x4*>(zs + j);
+    if (j + 4 <= nst) {
+      __builtin_amdgcn_raw_buffer_store_b128(v, ro, 4 * j, 0, 0);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) __builtin_amdgcn_raw_buffer_store_b32(v[e], ro, 4 * (j + e), 0, 0);
+    }
+    if constexpr (HIST) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = j + e < fill;
+        const uint32_t kb = zh_bin(a, v[e], lane);
+        atomicAdd(H.bins + kb, in ? 1u : 0u);
+        if (__builtin_expect(__ballot(in && kb == (uint32_t)ZH_TRASH) != 0, 0)) {
+          if (in && kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v[e], 1u);
+        }
+      }
+    }
+  }
+#else
   for (int j0 = 0; j0 < fill; j0 += 64) {
     const int j = j0 + lane;
     const int32_t v = zs[j];
@@ -990,6 +1019,7 @@ __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* o
       }
     }
   }
+#endif
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -1964,7 +1994,10 @@ hipError_t launch_intra_encode_luma(const uint8_t* img, int64_t nframes, int64_t
 // Exits at once when the count pass met a value outside int16 (*zr_cbad): the fused emission
 // pass runs instead.
 template <int C, bool DUP, bool HIST, int NG>
-__global__ __launch_bounds__(256) void sym_emit_kernel(FusedArgs a, int64_t ngroups) {
+__global__ __launch_bounds__(256) void sym_emit_kernel(FusedArgs a, int64_t ngroups,
+                                                       const int32_t* __restrict__ gcounts,
+                                                       const int64_t* __restrict__ goffs,
+                                                       const uint8_t* __restrict__ gflags) {
   constexpr int NP = (C == 1 && DUP) ? 2 : 3;
   constexpr int S8 = c8_stride(NP);
   __shared__ __attribute__((aligned(16))) int32_t win[4 * ZR_WIN];
@@ -1981,34 +2014,62 @@ __global__ __launch_bounds__(256) void sym_emit_kernel(FusedArgs a, int64_t ngro
   int32_t* os = win + wave * ZR_WIN;
   const int64_t nw = (int64_t)gridDim.x * 4;
   typedef int i32x4 __attribute__((ext_vector_type(4)));
-  for (int64_t gid = (int64_t)blockIdx.x * 4 + wave; gid < ngroups; gid += nw) {
-    const int gcount = a.zr_counts[gid];
-    if (gcount == 0) continue;                                   // a group past the row's end
-    const int64_t gbase = a.zr_off[gid];
-    const int nb = group_loc<NG>(a, (uint32_t)(gid / NG), (int)(gid % NG)).nb;
-    int32_t xv[8][NP];
-    if (a.zr_cflag[gid] == 0) {
-      const i32x4* src = reinterpret_cast<const i32x4*>(a.zr_c8 + (gid * 64 + lane) * S8);
-      i32x4 w[S8 / 16];
+  // a group's block column within its block row, kept incrementally (the count pass numbers
+  // the groups row by row: gid % (tpr NG) groups of 8 blocks from the row's start)
+  const int gpr = a.tpr * NG;
+  const int64_t gid0 = (int64_t)blockIdx.x * 4 + wave;
+  int gx = (int)(gid0 % gpr);
+  const int gstep = (int)(nw % gpr);
+  // the next group's count, offset, flag word and int8 coefficients are loaded while this
+  // group is emitted
+  struct Pre {
+    int count;
+    int64_t off;
+    uint32_t flagw;
+    i32x4 w[S8 / 16];
+  };
+  auto fetch = [&](int64_t gg, Pre& P) {
+    // (read-only, non-aliased kernel arguments: scalar loads, waited for at their first use
+    // in the next iteration, not right after the issue as uniform vector loads were)
+    P.count = gcounts[gg];
+    P.off = goffs[gg];
+    P.flagw = *reinterpret_cast<const uint32_t*>(gflags + (gg & ~(int64_t)3));
+    const i32x4* src = reinterpret_cast<const i32x4*>(a.zr_c8 + (gg * 64 + lane) * S8);
 #pragma unroll
-      for (int k = 0; k < S8 / 16; ++k) w[k] = __builtin_nontemporal_load(src + k);
+    for (int k = 0; k < S8 / 16; ++k) P.w[k] = __builtin_nontemporal_load(src + k);
+  };
+  Pre cur;
+  if (gid0 < ngroups) fetch(gid0, cur);
+  for (int64_t gid = gid0; gid < ngroups; gid += nw) {
+    Pre nxt;
+    if (gid + nw < ngroups) fetch(gid + nw, nxt);
+    const int gcount = cur.count;
+    const int nbl = a.w - 8 * gx;
+    const int nb = nbl < 0 ? 0 : (nbl < 8 ? nbl : 8);
+    gx += gstep;
+    if (gx >= gpr) gx -= gpr;
+    if (gcount != 0) {                                           // (0: a group past the row's end)
+      int32_t xv[8][NP];
+      if (((cur.flagw >> (8 * (gid & 3))) & 0xffu) == 0) {
 #pragma unroll
-      for (int e = 0; e < 8 * NP; ++e) {
-        const uint32_t word = (uint32_t)w[e / 16][(e / 4) & 3];
-        xv[e / NP][e % NP] = (int32_t)(int8_t)(uint8_t)(word >> (8 * (e & 3)));
+        for (int e = 0; e < 8 * NP; ++e) {
+          const uint32_t word = (uint32_t)cur.w[e / 16][(e / 4) & 3];
+          xv[e / NP][e % NP] = (int32_t)(int8_t)(uint8_t)(word >> (8 * (e & 3)));
+        }
+      } else {                                                   // rare: the group's int16 slot
+        const i32x4* src = reinterpret_cast<const i32x4*>(a.zr_c16 + (gid * 64 + lane) * S8);
+        i32x4 w[S8 / 8];
+#pragma unroll
+        for (int k = 0; k < S8 / 8; ++k) w[k] = src[k];
+#pragma unroll
+        for (int e = 0; e < 8 * NP; ++e) {
+          const uint32_t word = (uint32_t)w[e / 8][(e / 2) & 3];
+          xv[e / NP][e % NP] = (int32_t)(int16_t)(uint16_t)(word >> (16 * (e & 1)));
+        }
       }
-    } else {
-      const i32x4* src = reinterpret_cast<const i32x4*>(a.zr_c16 + (gid * 64 + lane) * S8);
-      i32x4 w[S8 / 8];
-#pragma unroll
-      for (int k = 0; k < S8 / 8; ++k) w[k] = src[k];
-#pragma unroll
-      for (int e = 0; e < 8 * NP; ++e) {
-        const uint32_t word = (uint32_t)w[e / 8][(e / 2) & 3];
-        xv[e / NP][e % NP] = (int32_t)(int16_t)(uint16_t)(word >> (16 * (e & 1)));
-      }
+      zr_emit_regs<C, DUP, HIST>(a, os, nb, cur.off, gcount, xv, hacc);
     }
-    zr_emit_regs<C, DUP, HIST>(a, os, nb, gbase, gcount, xv, hacc);
+    cur = nxt;
   }
   if constexpr (HIST) {
     __syncthreads();
@@ -2071,7 +2132,8 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
       auto k = a.zr_hist ? sym_emit_kernel<C, DUP, true, NG> : sym_emit_kernel<C, DUP, false, NG>;
       FusedArgs ae = a;
       ae.tpr = (int)tpr;                  // group_loc's tiles of NG groups, as the count pass
-      k<<<resident_grid(k, (ngroups + 3) / 4), 256, 0, s>>>(ae, ngroups);
+      k<<<resident_grid(k, (ngroups + 3) / 4), 256, 0, s>>>(ae, ngroups, ae.zr_counts, ae.zr_off,
+                                                            ae.zr_cflag);
       a.zr_gate = cbad;
     }
     if (a.zr_hist) launch_fused_zr<TI, C, DUP, CM, OUT_SYMH>(a, t, s);

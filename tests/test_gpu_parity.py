@@ -979,6 +979,49 @@ def test_zerorun_device_wide_and_general(nblk):
     assert torch.equal(off2, off) and np.array_equal(out2.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("tier", ["int8", "some_int16", "int32_value", "int16_slots_full"])
+def test_zerorun_int8_handoff_tiers(tier):
+    """The dense-row encoder hands the coefficients from its count pass to its emission pass
+    as int8, a group with a value outside int8 as int16 (side slots for 1 in 8 groups), and
+    falls back to emitting from the int32 rows when a value lies outside int16 or the int16
+    slots run out: every tier gives the oracle's stream and offsets."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    nblk = 16 * 2000 + 3
+    rng = np.random.default_rng(hash(tier) % 1000)
+    x = rng.integers(-100, 101, (nblk, 64)).astype(np.int32)
+    x[rng.random((nblk, 64)) > rng.random((nblk, 1))] = 0
+    x[-1, 63] = 127
+    x[-2, 0] = -128
+    if tier == "some_int16":           # 60 groups with values in [128, 32767]
+        g = rng.choice(nblk // 16, 60, replace=False)
+        x[g * 16 + 5, 7] = 32767
+        x[g * 16 + 9, 63] = -32768
+        x[g * 16 + 2, 0] = 128
+    elif tier == "int32_value":
+        x[777, 30] = 40000
+    elif tier == "int16_slots_full":   # every group wide: more than the side slots
+        x[::16, 1] = 300
+    want = O.zerorun_encode_fast(x)
+    blocks = torch.from_numpy(x).cuda()
+    off = torch.full((nblk + 1,), -7, dtype=torch.int64, device="cuda")
+    out = torch.full((want.size + 2,), -1, dtype=torch.int32, device="cuda")
+    D.zerorun_encode(blocks, off, out)
+    torch.cuda.synchronize()
+    o = off.cpu().numpy()
+    assert o[-1] == want.size
+    got = out.cpu().numpy()
+    assert np.array_equal(got[:want.size], want) and (got[want.size:] == -1).all()
+    # offsets: every block's slice ends with its EOB and holds its symbol count
+    nz = x != 0
+    last = np.where(nz.any(1), 63 - np.argmax(nz[:, ::-1], axis=1), -1)
+    zeros = ~nz & (np.arange(64)[None] <= last[:, None])
+    starts = zeros & ~np.concatenate([np.zeros((nblk, 1), bool), zeros[:, :-1]], axis=1)
+    cnt = nz.sum(1) + 2 * starts.sum(1) + 1
+    assert np.array_equal(o, np.concatenate([[0], np.cumsum(cnt)]))
+    assert (got[o[1:] - 1] == 4000).all()
+
+
 @pytest.mark.parametrize("shift", [1, 2, 3])
 def test_zerorun_device_unaligned_stream(shift):
     """The wide path's 16-byte stream stores when the caller's output starts 4, 8 or 12 bytes
