@@ -353,14 +353,42 @@ __device__ __forceinline__ zv4 zw_load(const int32_t* src, int64_t nblk, int64_t
   return __builtin_nontemporal_load(reinterpret_cast<const zv4*>(src + blk * 64) + (lane & 15));
 }
 
+// ---- dense rows through an int8 hand-off (r04) -------------------------------------------
+// The two passes below read the 256-byte rows twice (count, emit).  With the hand-off the
+// count pass (zw_count_kernel<true>) also stores each group's coefficients as int8 in its own
+// register layout — lane (i, q)'s 16 bytes = coefficients 4i .. 4i + 3 of blocks q, 4 + q,
+// 8 + q, 12 + q — or, for a group with a value outside int8, as int16 in a slot of a small side
+// area.  The emission pass (zc_emit_kernel) reads 1 KB per group instead of 4 KB, turns it into
+// lane k = coefficient k with one ds_bpermute per block, and places every block's symbols with
+// ballot/mbcnt into the wave's LDS window, then stores the group's contiguous range.  A value
+// outside int16 (or the int16 slots running out) sets `bad`: the emitter stands down and
+// zw_emit_kernel runs from the int32 rows instead (gated on the device).
+#ifndef IVC_ZC
+#define IVC_ZC 1
+#endif
+#ifndef IVC_ZC_NT
+#define IVC_ZC_NT 1
+#endif
+constexpr int ZC_BLK = 16;
+constexpr int ZC_WIN = 1664;   // words per wave: the group's <= 16 x 97 symbols + 65 dummy words
+
+struct ZcScratch {
+  uint8_t* c8;       // [ng][64 lanes][16 B], byte 4u + e = coefficient 4i + e of block 4u + q
+  uint8_t* c16;      // [cap16][64 lanes][32 B], int16 j the same value as byte j
+  int32_t* flag;     // [ng]: 0, or the group's int16 slot + 1
+  int32_t* ctl;      // [0] int16 slots taken, [1] bad
+  int64_t cap16;
+};
+
 // The wide path scans per-ZW_BLK-block group counts (nblk / 16 int32 written and scanned,
 // not nblk); the emit pass derives each block's offset from its group's offset and the
 // counts of the group's earlier blocks, and writes offsets[blk] itself.
 #ifndef IVC_ZW_COUNT_GROUPS
 #define IVC_ZW_COUNT_GROUPS 4   // 16-block groups per wave-iteration of the count pass (4: -2%)
 #endif
+template <bool EXPORT>
 __global__ __launch_bounds__(256) void zw_count_kernel(const int32_t* __restrict__ src, int64_t nblk,
-                                                       int32_t* __restrict__ gcounts) {
+                                                       int32_t* __restrict__ gcounts, ZcScratch z) {
   constexpr int NGR = IVC_ZW_COUNT_GROUPS;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -376,14 +404,66 @@ __global__ __launch_bounds__(256) void zw_count_kernel(const int32_t* __restrict
 #pragma unroll
       for (int l = 0; l < ZW_LOADS; ++l) {
         const int u = g * ZW_LOADS + l;
-        const ZwMask z = zw_mask(x[u], lane);
-        const int c = b0 + 4 * u + (lane >> 4) < nblk ? z.cnt : 0;
+        const ZwMask zm = zw_mask(x[u], lane);
+        const int c = b0 + 4 * u + (lane >> 4) < nblk ? zm.cnt : 0;
         // lanes 0, 16, 32, 48 hold the load's four blocks
         tot += __builtin_amdgcn_readlane(c, 0) + __builtin_amdgcn_readlane(c, 16) +
                __builtin_amdgcn_readlane(c, 32) + __builtin_amdgcn_readlane(c, 48);
       }
       const int64_t gi = b0 / ZW_BLK + g;
       if (lane == 0 && gi < ng) gcounts[gi] = tot;
+      if constexpr (EXPORT) {
+        if (gi < ng) {                                        // wave-uniform
+          // (blocks past nblk in the last group hold the last block's values: never emitted)
+          int32_t vlo = INT32_MAX, vhi = INT32_MIN;
+          uint32_t w8[ZW_LOADS];
+#pragma unroll
+          for (int l = 0; l < ZW_LOADS; ++l) {
+            const zv4 v = x[g * ZW_LOADS + l];
+            w8[l] = ((uint32_t)v.x & 0xffu) | ((uint32_t)v.y & 0xffu) << 8 |
+                    ((uint32_t)v.z & 0xffu) << 16 | ((uint32_t)v.w & 0xffu) << 24;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              vlo = min(vlo, v[e]);
+              vhi = max(vhi, v[e]);
+            }
+          }
+          const bool wide = vlo < -128 || vhi > 127, wider = vlo < -32768 || vhi > 32767;
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#if IVC_ZC_NT
+          __builtin_nontemporal_store(u32x4{w8[0], w8[1], w8[2], w8[3]},
+                                      reinterpret_cast<u32x4*>(z.c8 + (gi * 64 + lane) * 16));
+#else
+          *reinterpret_cast<u32x4*>(z.c8 + (gi * 64 + lane) * 16) = u32x4{w8[0], w8[1], w8[2], w8[3]};
+#endif
+          int flag = 0;
+          if (__ballot(wide)) {                               // wave-uniform, rare
+            if (__ballot(wider)) {
+              if (lane == 0) atomicOr(z.ctl + 1, 1);
+            } else {
+              int slot = 0;
+              if (lane == 0) slot = atomicAdd(z.ctl, 1);
+              slot = __shfl(slot, 0);
+              if (slot < z.cap16) {
+                uint32_t w16[2 * ZW_LOADS];
+#pragma unroll
+                for (int l = 0; l < ZW_LOADS; ++l) {
+                  const zv4 v = x[g * ZW_LOADS + l];
+                  w16[2 * l] = ((uint32_t)v.x & 0xffffu) | ((uint32_t)v.y & 0xffffu) << 16;
+                  w16[2 * l + 1] = ((uint32_t)v.z & 0xffffu) | ((uint32_t)v.w & 0xffffu) << 16;
+                }
+                u32x4* d16 = reinterpret_cast<u32x4*>(z.c16 + ((int64_t)slot * 64 + lane) * 32);
+                d16[0] = u32x4{w16[0], w16[1], w16[2], w16[3]};
+                d16[1] = u32x4{w16[4], w16[5], w16[6], w16[7]};
+                flag = slot + 1;
+              } else if (lane == 0) {
+                atomicOr(z.ctl + 1, 1);
+              }
+            }
+          }
+          if (lane == 0) z.flag[gi] = flag;
+        }
+      }
     }
   }
 }
@@ -492,99 +572,6 @@ __global__ __launch_bounds__(256) void zw_emit_kernel(const int32_t* __restrict_
   }
 }
 
-// ---- dense rows through an int8 hand-off (r04) -------------------------------------------
-// The two passes above read the 256-byte rows twice (count, emit).  Here the count pass
-// (zc_count_kernel: one wave per group of ZC_BLK = 16 blocks, lane k = coefficient k, so a
-// block's nonzero mask is one ballot and its count scalar bit operations) also stores the
-// group's coefficients as int8 — lane k's 16 bytes = coefficient k of the 16 blocks — or, for
-// a group with a value outside int8, as int16 in a slot of a small side area.  The emission
-// pass (zc_emit_kernel) reads 1 KB per group instead of 4 KB and places every block's symbols
-// with ballot/mbcnt into the wave's LDS window, then stores the group's contiguous range.
-// A value outside int16 (or the int16 slots running out) sets `bad`: the emitter stands down
-// and zw_emit_kernel runs from the int32 rows instead (gated on the device).
-#ifndef IVC_ZC
-#define IVC_ZC 0
-#endif
-constexpr int ZC_BLK = 16;
-constexpr int ZC_WIN = 1664;   // words per wave: the group's <= 16 x 97 symbols + 65 dummy words
-
-struct ZcScratch {
-  uint8_t* c8;       // [ng][64 lanes][16 B]
-  uint8_t* c16;      // [cap16][64 lanes][32 B]
-  int32_t* flag;     // [ng]: 0, or the group's int16 slot + 1
-  int32_t* ctl;      // [0] int16 slots taken, [1] bad
-  int64_t cap16;
-};
-
-__global__ __launch_bounds__(256) void zc_count_kernel(const int32_t* __restrict__ src, int64_t nblk,
-                                                       int32_t* __restrict__ gcounts, ZcScratch z) {
-  const int lane = threadIdx.x & 63;
-  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  const int64_t ng = (nblk + ZC_BLK - 1) / ZC_BLK;
-  // the next group's rows are loaded while this group is counted and packed
-  auto load = [&](int64_t g, int32_t (&x)[ZC_BLK]) {
-    const int64_t b0 = g * ZC_BLK;
-    const int nb = (int)(nblk - b0 < ZC_BLK ? nblk - b0 : ZC_BLK);
-#pragma unroll
-    for (int b = 0; b < ZC_BLK; ++b)
-      x[b] = b < nb ? __builtin_nontemporal_load(src + (b0 + b) * 64 + lane) : 0;
-  };
-  int32_t cur[ZC_BLK];
-  if (wave < ng) load(wave, cur);
-  for (int64_t g = wave; g < ng; g += nw) {
-    int32_t nxt[ZC_BLK];
-    if (g + nw < ng) load(g + nw, nxt);
-    const int nb = (int)(nblk - g * ZC_BLK < ZC_BLK ? nblk - g * ZC_BLK : ZC_BLK);
-    int total = 0;
-    bool wide = false, wider = false;
-#pragma unroll
-    for (int b = 0; b < ZC_BLK; ++b) {
-      const uint64_t m = __ballot(cur[b] != 0);
-      const int lz = m ? __builtin_clzll(m) : 64;
-      const uint64_t inside = m ? ~0ull >> lz : 0ull;       // bits [0, last nonzero]
-      const uint64_t zeros = ~m & inside;
-      const uint64_t st = zeros & ~(zeros << 1);            // run starts
-      total += b < nb ? __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1 : 0;
-      wide |= (uint32_t)(cur[b] + 128) > 255u;
-      wider |= (uint32_t)(cur[b] + 32768) > 65535u;
-    }
-    if (lane == 0) gcounts[g] = total;
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    uint32_t w8[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      w8[k] = ((uint32_t)cur[4 * k] & 0xffu) | ((uint32_t)cur[4 * k + 1] & 0xffu) << 8 |
-              ((uint32_t)cur[4 * k + 2] & 0xffu) << 16 | ((uint32_t)cur[4 * k + 3] & 0xffu) << 24;
-    *reinterpret_cast<u32x4*>(z.c8 + (g * 64 + lane) * 16) = u32x4{w8[0], w8[1], w8[2], w8[3]};
-    int flag = 0;
-    if (__ballot(wide)) {                                     // wave-uniform, rare
-      if (__ballot(wider)) {
-        if (lane == 0) atomicOr(z.ctl + 1, 1);
-      } else {
-        int slot = 0;
-        if (lane == 0) slot = atomicAdd(z.ctl, 1);
-        slot = __shfl(slot, 0);
-        if (slot < z.cap16) {
-          uint32_t w16[8];
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-            w16[k] = ((uint32_t)cur[2 * k] & 0xffffu) | ((uint32_t)cur[2 * k + 1] & 0xffffu) << 16;
-          u32x4* d16 = reinterpret_cast<u32x4*>(z.c16 + ((int64_t)slot * 64 + lane) * 32);
-          d16[0] = u32x4{w16[0], w16[1], w16[2], w16[3]};
-          d16[1] = u32x4{w16[4], w16[5], w16[6], w16[7]};
-          flag = slot + 1;
-        } else if (lane == 0) {
-          atomicOr(z.ctl + 1, 1);
-        }
-      }
-    }
-    if (lane == 0) z.flag[g] = flag;
-#pragma unroll
-    for (int b = 0; b < ZC_BLK; ++b) cur[b] = nxt[b];
-  }
-}
-
 // one wave per group; the block offsets off[blk] are written here (the scan wrote the group
 // offsets and the stream length)
 __global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
@@ -621,18 +608,26 @@ __global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
     Pre nxt;
     if (g + nw < ng) fetch(g + nw, nxt);
     const int nb = (int)(nblk - g * ZC_BLK < ZC_BLK ? nblk - g * ZC_BLK : ZC_BLK);
+    // lane k = coefficient k: block 4u + q's value comes from lane (k >> 2) + 16 q, dword u,
+    // byte k & 3 (one ds_bpermute per block)
     int32_t xv[ZC_BLK];
+    const int sel = (lane >> 2) * 4;
     if (cur.flag == 0) {
 #pragma unroll
-      for (int e = 0; e < ZC_BLK; ++e)
-        xv[e] = (int32_t)(int8_t)(uint8_t)((uint32_t)cur.w[e / 4] >> (8 * (e & 3)));
+      for (int b = 0; b < ZC_BLK; ++b) {
+        const int v = __builtin_amdgcn_ds_bpermute(sel + 64 * (b & 3), cur.w[b >> 2]);
+        xv[b] = __builtin_amdgcn_sbfe(v, 8 * (lane & 3), 8);
+      }
     } else {                                                  // rare: the group's int16 slot
       const i32x4* src = reinterpret_cast<const i32x4*>(c16 + ((int64_t)(cur.flag - 1) * 64 + lane) * 32);
       const i32x4 a0 = src[0], a1 = src[1];
+      const int d[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
 #pragma unroll
-      for (int e = 0; e < ZC_BLK; ++e) {
-        const uint32_t word = (uint32_t)(e < 8 ? a0[e / 2] : a1[(e - 8) / 2]);
-        xv[e] = (int32_t)(int16_t)(uint16_t)(word >> (16 * (e & 1)));
+      for (int b = 0; b < ZC_BLK; ++b) {
+        const int u = b >> 2;
+        const int lo = __builtin_amdgcn_ds_bpermute(sel + 64 * (b & 3), d[2 * u]);
+        const int hi = __builtin_amdgcn_ds_bpermute(sel + 64 * (b & 3), d[2 * u + 1]);
+        xv[b] = __builtin_amdgcn_sbfe((lane & 2) ? hi : lo, 16 * (lane & 1), 16);
       }
     }
     int fill = 0, offv = 0;
@@ -651,12 +646,17 @@ __global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
       const bool pnz = __builtin_amdgcn_inverse_ballot_w64(pm);
       const bool rs = __builtin_amdgcn_inverse_ballot_w64(st);
       const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
-      const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
-                      2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
+      // the lane's slot, fill included (mbcnt accumulates: m's bits below the lane, st's twice)
+      uint32_t slot = __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)fill);
+      slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), slot);
+      slot = __builtin_amdgcn_mbcnt_lo((uint32_t)st, slot);
+      slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), slot);
+      slot = __builtin_amdgcn_mbcnt_lo((uint32_t)st, slot);
+      slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), slot);
       const bool w1 = nz || pnz;
       const int32_t v1 = nz || hl ? x : eob;
       const int32_t v2 = rs ? (int32_t)__builtin_ctzll(later) : eob;
-      int32_t* const d = w1 ? os + fill + pos : dummy;
+      int32_t* const d = w1 ? os + slot : dummy;
       d[1] = v2;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // keep the two writes ordered
       d[0] = v1;
@@ -764,9 +764,11 @@ hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, 
     if (IVC_ZC) {
       hipError_t e = hipMemsetAsync(z.zc.ctl, 0, 8, s);
       if (e != hipSuccess) return e;
-      zc_count_kernel<<<zw_grid(nblk, 8), 256, 0, s>>>(src, nblk, z.counts, z.zc);
+      zw_count_kernel<true><<<zw_grid((nblk + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(
+          src, nblk, z.counts, z.zc);
     } else {
-      zw_count_kernel<<<zw_grid((nblk + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(src, nblk, z.counts);
+      zw_count_kernel<false><<<zw_grid((nblk + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(
+          src, nblk, z.counts, z.zc);
     }
     return device_scan<int64_t>(ng, CountGen{z.counts}, SumI64{}, GroupOffsetSink{z.goff, ng, off + nblk},
                                 z.agg, s);
@@ -940,16 +942,25 @@ constexpr int ZF_TILE = 4096, ZF_HALO = 128;
 // the symbols -> image path locates its groups from it)
 // The next tile's loads are issued before this tile is counted (a wave has 8 KB of reads in
 // flight instead of 4: one load latency per tile measured 3.3 ms for the cfg3 stream, 4.3 TB/s).
+#ifndef IVC_ZF_WAVE_CONTIG
+#define IVC_ZF_WAVE_CONTIG 0
+#endif
+// symbol offset inside the tile of lane `lane` of wave w at step k: IVC_ZF_WAVE_CONTIG gives
+// each wave a contiguous quarter of the tile (the symbol before a lane-0 quad at k > 0 is then
+// lane 63's last of step k - 1, taken by readlane; one scalar load per tile instead of 4)
+__device__ __forceinline__ int zf_off(int w, int k, int lane) {
+  return IVC_ZF_WAVE_CONTIG ? w * (ZF_TILE / 4) + k * 256 + lane * 4 : (k * 256 + w * 64 + lane) * 4;
+}
 struct ZfTile {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   i32x4 q[ZF_TILE / 1024];
   int p0[ZF_TILE / 1024];
 };
 __device__ __forceinline__ void zf_load_tile(const int32_t* __restrict__ s, int64_t n, int64_t t,
-                                             int tid, ZfTile& T) {
+                                             int w, int lane, ZfTile& T) {
 #pragma unroll
   for (int k = 0; k < ZF_TILE / 1024; ++k) {
-    const int64_t i = t * ZF_TILE + (int64_t)(k * 256 + tid) * 4;
+    const int64_t i = t * ZF_TILE + zf_off(w, k, lane);
     if (i + 3 < n) {
       T.q[k] = __builtin_nontemporal_load(reinterpret_cast<const ZfTile::i32x4*>(s + i));
     } else {
@@ -959,28 +970,36 @@ __device__ __forceinline__ void zf_load_tile(const int32_t* __restrict__ s, int6
     // the symbol before the wave's first: one scalar load per wave (a wave-uniform address),
     // issued with the quads — not a per-lane load (one dword load per lane doubled the vector
     // memory instructions), nor a lane-0 vector load after the quad (a second latency)
-    const int64_t iw = (int64_t)__builtin_amdgcn_readfirstlane((int)(i - t * ZF_TILE)) + t * ZF_TILE;
-    T.p0[k] = iw > 0 && iw <= n ? s[iw - 1] : 1;   // the stream's first slot is a value slot
+    if (!IVC_ZF_WAVE_CONTIG || k == 0) {
+      const int64_t iw = t * ZF_TILE + zf_off(w, k, 0);
+      T.p0[k] = iw > 0 && iw <= n ? s[iw - 1] : 1;   // the stream's first slot is a value slot
+    }
   }
 }
 __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict__ s, int64_t n,
                                                        int32_t eob, int32_t* __restrict__ tile_eobs,
                                                        int* fail, uint32_t* __restrict__ eobmask) {
   const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int64_t ntiles = (n + ZF_TILE - 1) / ZF_TILE;
   ZfTile cur;
-  if ((int64_t)blockIdx.x < ntiles) zf_load_tile(s, n, blockIdx.x, tid, cur);
+  if ((int64_t)blockIdx.x < ntiles) zf_load_tile(s, n, blockIdx.x, w, lane, cur);
   for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
     ZfTile nxt;
-    if (t + gridDim.x < ntiles) zf_load_tile(s, n, t + gridDim.x, tid, nxt);
+    if (t + gridDim.x < ntiles) zf_load_tile(s, n, t + gridDim.x, w, lane, nxt);
     int cnt = 0;
     bool bad = false;
+    int last = cur.p0[0];                    // (IVC_ZF_WAVE_CONTIG) the symbol before step k
 #pragma unroll
     for (int k = 0; k < ZF_TILE / 1024; ++k) {
-      const int64_t i = t * ZF_TILE + (int64_t)(k * 256 + tid) * 4;
+      const int off = zf_off(w, k, lane);
+      const int64_t i = t * ZF_TILE + off;
       const int v[4] = {cur.q[k].x, cur.q[k].y, cur.q[k].z, cur.q[k].w};
-      // the symbol before: the previous lane's last (DPP), lane 0's from the scalar load
-      int pv = __builtin_amdgcn_update_dpp(cur.p0[k], v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
+      // the symbol before: the previous lane's last (DPP), lane 0's from the scalar load or
+      // the previous step's lane 63
+      const int p0 = IVC_ZF_WAVE_CONTIG ? last : cur.p0[k];
+      int pv = __builtin_amdgcn_update_dpp(p0, v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
+      if (IVC_ZF_WAVE_CONTIG) last = __builtin_amdgcn_readlane(v[3], 63);
       uint32_t bits = 0;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -994,17 +1013,23 @@ __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict
       }
       if (eobmask) {
         // 8 lanes' nibbles make one word: OR by DPP (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror)
-        bits <<= 4 * (tid & 7);
+        bits <<= 4 * (lane & 7);
         bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);
         bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xf, 0xf, false);
         bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x141, 0xf, 0xf, false);
-        if ((tid & 7) == 0) eobmask[t * (ZF_TILE / 32) + (k * 256 + tid) / 8] = bits;
+        if ((lane & 7) == 0) eobmask[t * (ZF_TILE / 32) + off / 32] = bits;
       }
     }
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d);
+    // the wave's count by DPP (no LDS: an LDS wait would also wait for the prefetched scalar load)
+    cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x111, 0xf, 0xf, false);   // row_shr:1
+    cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x112, 0xf, 0xf, false);   // row_shr:2
+    cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x114, 0xf, 0xf, false);   // row_shr:4
+    cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x118, 0xf, 0xf, false);   // row_shr:8
+    cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    const int wc = __builtin_amdgcn_readlane(cnt, 63);
     if (__ballot(bad) && lane == 0) atomicOr(fail, 1);
-    if (lane == 0 && cnt) atomicAdd(tile_eobs + t, cnt);    // tile_eobs zeroed by the caller
+    if (lane == 0 && wc) atomicAdd(tile_eobs + t, wc);      // tile_eobs zeroed by the caller
     cur = nxt;
   }
 }

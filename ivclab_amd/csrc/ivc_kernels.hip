@@ -923,6 +923,24 @@ __device__ __forceinline__ uint32_t zh_bin(const FusedArgs& a, int32_t v, int la
 #ifndef IVC_EMIT_FLUSH4
 #define IVC_EMIT_FLUSH4 0
 #endif
+#ifndef IVC_EMIT_SLOT_CHAIN
+#define IVC_EMIT_SLOT_CHAIN 1
+#endif
+// a lane's emission slot: base + (bits of m below the lane) + 2 (bits of st below the lane)
+__device__ __forceinline__ int emit_slot(uint64_t m, uint64_t st, int base) {
+  uint32_t t = __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)base);
+  t = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), t);
+  t = __builtin_amdgcn_mbcnt_lo((uint32_t)st, t);
+  t = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), t);
+  t = __builtin_amdgcn_mbcnt_lo((uint32_t)st, t);
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), t);
+}
+#ifndef IVC_EMIT_TRASH_LATE
+#define IVC_EMIT_TRASH_LATE 0
+#endif
+#ifndef IVC_EMIT_FLUSH_SPLIT
+#define IVC_EMIT_FLUSH_SPLIT 1
+#endif
 template <int C, bool DUP, bool HIST>
 __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* os, int64_t gbase,
                                                   int gcount, const int32_t (&xv)[8][(C == 1 && DUP) ? 2 : 3],
@@ -956,15 +974,25 @@ __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* o
       const uint64_t st = __ballot(rs);
 #endif
       const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
+#if IVC_EMIT_SLOT_CHAIN
+      // the lane's slot, fill included: mbcnt accumulates, so m's bits below the lane and st's
+      // twice chain into one value (no shifts or adds)
+      const int slot = emit_slot(m, st, fill);
+#else
       const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
                       2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
+#endif
       // a nonzero, a run's 0 + its length, or (the first zero after the last nonzero) the EOB
       const bool w1 = nz || pnz;
       const int32_t v1 = nz || hl ? x : eob;
       const int32_t v2 = rs ? (int32_t)__builtin_ctzll(later) : eob;
 #pragma unroll
       for (int k = 0; k < (p == 1 ? R1 : 1); ++k) {
+#if IVC_EMIT_SLOT_CHAIN
+        int32_t* const d = w1 ? zs + slot + (k ? cnt : 0) : zs + ZR_WIN - 65 + lane;
+#else
         int32_t* const d = w1 ? zs + fill + pos : zs + ZR_WIN - 65 + lane;
+#endif
         d[1] = v2;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // keep the two writes ordered
         d[0] = v1;
@@ -1002,6 +1030,59 @@ __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* o
         if (__builtin_expect(__ballot(in && kb == (uint32_t)ZH_TRASH) != 0, 0)) {
           if (in && kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v[e], 1u);
         }
+      }
+    }
+  }
+#elif IVC_EMIT_TRASH_LATE
+  // symbols outside the LDS bins (rare) are remembered per lane and added to the global
+  // histogram in a second walk over the still-intact window: no ballot and branch per 64
+  uint32_t trash = 0;
+  for (int j0 = 0; j0 < fill; j0 += 64) {
+    const int j = j0 + lane;
+    const int32_t v = zs[j];
+    __builtin_amdgcn_raw_buffer_store_b32(v, ro, 4 * j, 0, 0);
+    if constexpr (HIST) {
+      const uint32_t w = j < fill ? 1u : 0u;
+      const uint32_t kb = zh_bin(a, v, lane);
+      atomicAdd(H.bins + kb, w);
+      trash |= kb == (uint32_t)ZH_TRASH ? w : 0u;             // (VALU: no mask merging)
+    }
+  }
+  if constexpr (HIST) {
+    if (__builtin_expect(__ballot(trash != 0u) != 0, 0)) {
+      for (int j0 = 0; j0 < fill; j0 += 64) {
+        const int j = j0 + lane;
+        const int32_t v = zs[j];
+        if (j < fill && zh_bin(a, v, lane) == (uint32_t)ZH_TRASH) zr_hist_global(a, v, 1u);
+      }
+    }
+  }
+#elif IVC_EMIT_FLUSH_SPLIT
+  // whole 64-symbol rows without the weight test, then the partial row (the row offset stays
+  // in the vector offset: the buffer range check that clips at the caller's capacity does not
+  // include the scalar offset)
+  const int nfull = fill >> 6;
+#pragma unroll 4
+  for (int r = 0; r < nfull; ++r) {
+    const int32_t v = zs[64 * r + lane];
+    __builtin_amdgcn_raw_buffer_store_b32(v, ro, 4 * (64 * r + lane), 0, 0);
+    if constexpr (HIST) {
+      const uint32_t kb = zh_bin(a, v, lane);
+      atomicAdd(H.bins + kb, 1u);
+      if (__builtin_expect(__ballot(kb == (uint32_t)ZH_TRASH) != 0, 0)) {
+        if (kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v, 1u);
+      }
+    }
+  }
+  if (fill & 63) {
+    const int32_t v = zs[64 * nfull + lane];
+    __builtin_amdgcn_raw_buffer_store_b32(v, ro, 4 * (64 * nfull + lane), 0, 0);
+    if constexpr (HIST) {
+      const bool in = lane < (fill & 63);
+      const uint32_t kb = zh_bin(a, v, lane);
+      atomicAdd(H.bins + kb, in ? 1u : 0u);
+      if (__builtin_expect(__ballot(in && kb == (uint32_t)ZH_TRASH) != 0, 0)) {
+        if (in && kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v, 1u);
       }
     }
   }
@@ -1139,16 +1220,17 @@ __device__ __forceinline__ void zr_export_coefs(const FusedArgs& a, const int32_
   constexpr int S8 = c8_stride(NP);
   const int lane = threadIdx.x & 63;
   int32_t v[8 * NP];
-  bool wide = false, wider = false;
+  int32_t vlo = INT32_MAX, vhi = INT32_MIN;                  // (min3/max3 chains: 2 VALU per 2 values)
 #pragma unroll
   for (int b = 0; b < 8; ++b)
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
       const int32_t x = os[b * PITCH + p * 64 + lane];
       v[b * NP + p] = x;
-      wide |= (uint32_t)(x + 128) > 255u;
-      wider |= (uint32_t)(x + 32768) > 65535u;
+      vlo = min(vlo, x);
+      vhi = max(vhi, x);
     }
+  const bool wide = vlo < -128 || vhi > 127, wider = vlo < -32768 || vhi > 32767;
   if (__ballot(wider) && lane == 0) atomicOr(a.zr_cbad, 1);
   uint32_t w8[S8 / 4];
 #pragma unroll
