@@ -1197,12 +1197,9 @@ int ivc_zerorun_encode_dev(const int32_t* src, int64_t nblk, int32_t row_stride,
     hipError_t e = scratch_alloc(&scratch, (size_t)zerorun_scratch_bytes(nblk), s);
     if (e != hipSuccess) return fail(IVC_E_NOMEM, std::string("hipMallocAsync: ") + hipGetErrorString(e));
   }
-  int rc = dev_launch(launch_zerorun_offsets(src, nblk, row_stride, block_size, scratch, offsets, s),
-                      "zerorun_encode");
-  if (!rc)
-    rc = dev_launch(launch_zerorun_emit(src, nblk, row_stride, block_size, eob, scratch, offsets, out,
-                                        capacity, s),
-                    "zerorun_encode");
+  const int rc = dev_launch(launch_zerorun_encode(src, nblk, row_stride, block_size, eob, scratch,
+                                                  offsets, out, capacity, s),
+                            "zerorun_encode");
   if (scratch) (void)hipFreeAsync(scratch, s);
   return rc;
 }

@@ -310,7 +310,8 @@ constexpr int SYM_XW = SYM_SEG + 8;                    // int32 words: [3] = pre
 constexpr int SYM_XD = (SYM_XW / 2 > DX_WAVE ? SYM_XW / 2 : DX_WAVE);   // doubles per wave
 
 template <int C, bool RGB, int DQM>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void sym_image_kernel(DecArgs a, SymImageArgs z, QTab t,
+                                                                                              const int64_t* grange) {
   constexpr int QS = 8 * C * SYM_QP;                   // int16 per wave
   __shared__ __attribute__((aligned(16))) int16_t qs_all[4 * QS];
   __shared__ int bps_all[4 * 32];                       // block-plane start offsets per wave
@@ -330,13 +331,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   int32_t* st = reinterpret_cast<int32_t*>(xs) + 4;    // st[-1]: the symbol before the round
   const int64_t nw = (int64_t)gridDim.x * 4;
   bool bad = false;
+  // groups [g_lo, g_hi): all, or one chunk of a pipelined call (grange, written on the device)
+  const int64_t g_lo = grange ? grange[0] : 0, g_hi = grange ? grange[1] : a.ngroups;
   // the group bounds are loaded one group ahead (scalar loads in flight during the group)
-  int64_t g = (int64_t)blockIdx.x * 4 + wave;
-  int64_t Sn = g < a.ngroups ? z.gstart[g] : 0, En = g < a.ngroups ? z.gstart[g + 1] : 0;
-  for (; g < a.ngroups; g += nw) {
+  int64_t g = g_lo + (int64_t)blockIdx.x * 4 + wave;
+  int64_t Sn = g < g_hi ? z.gstart[g] : 0, En = g < g_hi ? z.gstart[g + 1] : 0;
+  for (; g < g_hi; g += nw) {
     const DecGroup G = dec_group<DEC_IMAGE>(a, g);
     const int64_t S = Sn, E = En;
-    if (g + nw < a.ngroups) {
+    if (g + nw < g_hi) {
       Sn = z.gstart[g + nw];
       En = z.gstart[g + nw + 1];
     }
@@ -477,14 +480,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
 // The stream start is group 0's, the position after the last expected EOB is gstart[ngroups].
 __global__ __launch_bounds__(256) void sym_locate_kernel(const uint32_t* __restrict__ mask,
                                                          const int64_t* __restrict__ tile_first,
-                                                         int64_t ntiles, int C, int w, int gpr,
-                                                         int64_t nbp_total, int64_t* gstart) {
+                                                         int64_t t_begin, int64_t ntiles, int C,
+                                                         int w, int gpr, int64_t nbp_total,
+                                                         int64_t* gstart) {
   const int lane = threadIdx.x & 63;
   const int64_t nwv = (int64_t)gridDim.x * 4;
-  if (blockIdx.x == 0 && threadIdx.x == 0) gstart[0] = 0;
+  if (t_begin == 0 && blockIdx.x == 0 && threadIdx.x == 0) gstart[0] = 0;
   const int64_t D = (int64_t)C * w;                    // block-planes per block row
   const int64_t GS = 8 * (int64_t)C;                   // block-planes per full group
-  for (int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntiles; t += nwv) {
+  for (int64_t t = t_begin + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); t < ntiles; t += nwv) {
     const uint64_t mk = (uint64_t)mask[t * 128 + 2 * lane] | ((uint64_t)mask[t * 128 + 2 * lane + 1] << 32);
     const int cnt = __builtin_popcountll(mk);
     const int incl = dec_wave_incl_sum(cnt);
@@ -563,11 +567,10 @@ hipError_t launch_intra_decode_image(const int32_t* q, int64_t nframes, int64_t 
 #undef DEC_IMG
 }
 
-// symbols -> image, fused: gstart from the EOB mask, then the group kernel (see above)
-hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const uint32_t* eobmask,
-                            const int64_t* tile_first, int64_t ntiles, int64_t nframes, int64_t H,
-                            int64_t W, int C, const QTab& t, int to_rgb, double* out,
-                            int64_t* gstart, int* fail, hipStream_t s) {
+// symbols -> image, fused: gstart from the EOB mask, then the group kernel (see above).
+// The pipelined call (launch_symbols2image) runs both per chunk of tiles: locate_range on
+// tiles [t0, t1), image_range on the groups of a device-written range.
+static DecArgs s2i_args(int64_t nframes, int64_t H, int64_t W, double* out) {
   DecArgs a{};
   a.out = out;
   a.w = (int)(W / 8);
@@ -575,17 +578,60 @@ hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const ui
   a.nblk = nframes * (H / 8) * a.w;
   a.ngroups = nframes * (H / 8) * a.gpr;
   a.W3 = W * 3;
-  hipError_t e = hipMemsetAsync(gstart, 0xff, (size_t)(a.ngroups + 1) * 8, s);
-  if (e != hipSuccess) return e;
-  {
-    const int64_t nb = (ntiles + 3) / 4;
-    sym_locate_kernel<<<(unsigned)(nb < 256 * 16 ? (nb > 0 ? nb : 1) : 256 * 16), 256, 0, s>>>(
-        eobmask, tile_first, ntiles, C, a.w, a.gpr, (int64_t)C * a.nblk, gstart);
-  }
+  return a;
+}
+
+hipError_t launch_sym_locate_range(const uint32_t* eobmask, const int64_t* tile_first, int64_t t0,
+                                   int64_t t1, int64_t nframes, int64_t H, int64_t W, int C,
+                                   int64_t* gstart, hipStream_t s) {
+  const DecArgs a = s2i_args(nframes, H, W, nullptr);
+  const int64_t nb = (t1 - t0 + 3) / 4;
+  if (nb <= 0) return hipSuccess;
+  sym_locate_kernel<<<(unsigned)(nb < 256 * 16 ? nb : 256 * 16), 256, 0, s>>>(
+      eobmask, tile_first, t0, t1, C, a.w, a.gpr, (int64_t)C * a.nblk, gstart);
+  return hipGetLastError();
+}
+
+// the groups chunk c owns: those whose first block-plane follows an EOB of the chunk's tiles,
+// i.e. first block-plane in [E_c + 1, E_{c+1} + 1) with E = EOBs before the chunk (tile_first
+// at its first tile); chunk 0 also owns group 0, the last chunk every group to the end
+__global__ void s2i_group_range_kernel(const int64_t* tile_first, int64_t tc0, int64_t tc1,
+                                       int first, int last, int C, int w, int gpr,
+                                       int64_t ngroups, int64_t* range) {
+  const int64_t D = (int64_t)C * w, GS = 8 * (int64_t)C;
+  auto first_group_from = [&](int64_t b) -> int64_t {   // first group whose first block-plane >= b
+    if (b <= 0) return 0;
+    int64_t row = b / D, rem = b - row * D;
+    rem = (rem + GS - 1) / GS * GS;
+    if (rem >= D) {
+      ++row;
+      rem = 0;
+    }
+    const int64_t g = row * gpr + rem / GS;
+    return g < ngroups ? g : ngroups;
+  };
+  range[0] = first ? 0 : first_group_from(tile_first[tc0] + 1);
+  range[1] = last ? ngroups : first_group_from(tile_first[tc1] + 1);
+}
+
+hipError_t launch_sym_group_range(const int64_t* tile_first, int64_t tc0, int64_t tc1, int first,
+                                  int last, int64_t nframes, int64_t H, int64_t W, int C,
+                                  int64_t* range, hipStream_t s) {
+  const DecArgs a = s2i_args(nframes, H, W, nullptr);
+  s2i_group_range_kernel<<<1, 1, 0, s>>>(tile_first, tc0, tc1, first, last, C, a.w, a.gpr,
+                                         a.ngroups, range);
+  return hipGetLastError();
+}
+
+hipError_t launch_sym_image_range(const int32_t* sym, int64_t n, int32_t eob, int64_t nframes,
+                                  int64_t H, int64_t W, int C, const QTab& t, int to_rgb,
+                                  double* out, const int64_t* gstart, int* fail,
+                                  const int64_t* grange, hipStream_t s) {
+  const DecArgs a = s2i_args(nframes, H, W, out);
   SymImageArgs z{sym, n, eob, gstart, fail};
   auto go = [&](auto k) {
     const unsigned grid = resident_grid_ptr(reinterpret_cast<const void*>(k), (a.ngroups + 3) / 4);
-    k<<<grid, 256, 0, s>>>(a, z, t);
+    k<<<grid, 256, 0, s>>>(a, z, t, grange);
   };
   // int16 coefficients times a finite table below 2^16 in magnitude stay inside int32 (and
   // with a table of positive integers the product is exact)
@@ -611,6 +657,20 @@ hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const ui
   if (to_rgb) pick(std::true_type{});
   else pick(std::false_type{});
   return hipGetLastError();
+}
+
+hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const uint32_t* eobmask,
+                            const int64_t* tile_first, int64_t ntiles, int64_t nframes, int64_t H,
+                            int64_t W, int C, const QTab& t, int to_rgb, double* out,
+                            int64_t* gstart, int* fail, hipStream_t s) {
+  const DecArgs a = s2i_args(nframes, H, W, out);
+  hipError_t e = hipMemsetAsync(gstart, 0xff, (size_t)(a.ngroups + 1) * 8, s);
+  if (e == hipSuccess)
+    e = launch_sym_locate_range(eobmask, tile_first, 0, ntiles, nframes, H, W, C, gstart, s);
+  if (e == hipSuccess)
+    e = launch_sym_image_range(sym, n, eob, nframes, H, W, C, t, to_rgb, out, gstart, fail,
+                               nullptr, s);
+  return e;
 }
 
 }  // namespace ivc

@@ -17,10 +17,42 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <algorithm>
+#include <mutex>
+#include <type_traits>
 
 #include "ivc_internal.h"
 
 namespace ivc {
+
+// A second stream (and events) per device for the pipelined calls (symbols2image, zero-run
+// encode): work on it is ordered against the caller's stream by events; the mutex serialises
+// the enqueue of concurrent host threads.
+constexpr int PIPE_EVENTS = 66;
+struct PipeCtx {
+  hipStream_t aux = nullptr;
+  hipEvent_t ev[PIPE_EVENTS] = {};
+  std::mutex mu;
+  bool ok = false;
+};
+static PipeCtx g_pipe[64];
+static std::once_flag g_pipe_once[64];
+static hipError_t pipe_ctx(PipeCtx** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
+  PipeCtx& P = g_pipe[dev];
+  std::call_once(g_pipe_once[dev], [&P] {
+    bool good = hipStreamCreateWithFlags(&P.aux, hipStreamNonBlocking) == hipSuccess;
+    for (auto& ev : P.ev)
+      good = good && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
+    P.ok = good;
+  });
+  if (!P.ok) return hipErrorNotInitialized;
+  *out = &P;
+  return hipSuccess;
+}
 
 // ---------------------------------------------------------------- generic tile scan ---
 // Exclusive scan of gen(i), i in [0, n), with an associative Op over T; sink(i, excl, v)
@@ -255,6 +287,19 @@ struct OffsetSink {
   }
 };
 
+// OffsetSink continuing a previous scan: every prefix plus *carry (the previous chunk's total,
+// which the previous scan wrote at off[0]; thread 0 rewrites that same value)
+struct OffsetCarrySink {
+  int64_t* off;
+  int64_t n;
+  const int64_t* carry;
+  __device__ void operator()(int64_t i, int64_t excl, int64_t v) const {
+    const int64_t c = *carry;
+    off[i] = excl + c;
+    if (i == n - 1) off[n] = excl + v + c;
+  }
+};
+
 __global__ __launch_bounds__(256) void zr_emit_kernel(const int32_t* __restrict__ src, int64_t nblk,
                                                       int stride, int B, int32_t eob,
                                                       const int64_t* __restrict__ off,
@@ -386,15 +431,18 @@ struct ZcScratch {
 #ifndef IVC_ZW_COUNT_GROUPS
 #define IVC_ZW_COUNT_GROUPS 4   // 16-block groups per wave-iteration of the count pass (4: -2%)
 #endif
+// groups [g_begin, g_end) (g_end < 0: all)
 template <bool EXPORT>
 __global__ __launch_bounds__(256) void zw_count_kernel(const int32_t* __restrict__ src, int64_t nblk,
-                                                       int32_t* __restrict__ gcounts, ZcScratch z) {
+                                                       int32_t* __restrict__ gcounts, ZcScratch z,
+                                                       int64_t g_begin = 0, int64_t g_end = -1) {
   constexpr int NGR = IVC_ZW_COUNT_GROUPS;
   const int lane = threadIdx.x & 63;
   const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
-  for (int64_t b0 = wave * ZW_BLK * NGR; b0 < nblk; b0 += nw * ZW_BLK * NGR) {
+  const int64_t ng_all = (nblk + ZW_BLK - 1) / ZW_BLK;
+  const int64_t ng = g_end < 0 || g_end > ng_all ? ng_all : g_end;
+  for (int64_t b0 = (g_begin + wave * NGR) * ZW_BLK; b0 < ng * ZW_BLK; b0 += nw * ZW_BLK * NGR) {
     zv4 x[NGR * ZW_LOADS];
 #pragma unroll
     for (int u = 0; u < NGR * ZW_LOADS; ++u) x[u] = zw_load(src, nblk, b0, u, lane);
@@ -581,13 +629,15 @@ __global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
                                                       const int32_t* __restrict__ gflag,
                                                       const int32_t* __restrict__ bad,
                                                       int64_t* __restrict__ off,
-                                                      int32_t* __restrict__ out, int64_t capacity) {
+                                                      int32_t* __restrict__ out, int64_t capacity,
+                                                      int64_t g_begin = 0, int64_t g_end = -1) {
   __shared__ __attribute__((aligned(16))) int32_t win[4 * ZC_WIN];
   if (*bad) return;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * 4;
-  const int64_t ng = (nblk + ZC_BLK - 1) / ZC_BLK;
+  const int64_t ng_all = (nblk + ZC_BLK - 1) / ZC_BLK;
+  const int64_t ng = g_end < 0 || g_end > ng_all ? ng_all : g_end;
   int32_t* const os = win + wave * ZC_WIN;
   int32_t* const dummy = os + ZC_WIN - 65 + lane;
   typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -601,7 +651,7 @@ __global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
     P.flag = gflag[g];
     P.w = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(c8 + (g * 64 + lane) * 16));
   };
-  const int64_t g0 = (int64_t)blockIdx.x * 4 + wave;
+  const int64_t g0 = g_begin + (int64_t)blockIdx.x * 4 + wave;
   Pre cur;
   if (g0 < ng) fetch(g0, cur);
   for (int64_t g = g0; g < ng; g += nw) {
@@ -689,6 +739,22 @@ static unsigned zw_grid(int64_t nblk, int per_cu) {
   if (grid > 256 * per_cu) grid = 256 * per_cu;
   return (unsigned)(grid < 1 ? 1 : grid);
 }
+
+// GroupOffsetSink continuing a previous chunk's scan (carry = its total, at goff[0] here)
+struct GroupOffsetCarrySink {
+  int64_t* goff;
+  int64_t ng;
+  const int64_t* carry;
+  int64_t* total;             // the stream length, written by the last chunk only
+  __device__ void operator()(int64_t i, int64_t excl, int64_t v) const {
+    const int64_t c = *carry;
+    goff[i] = excl + c;
+    if (i == ng - 1) {
+      goff[ng] = excl + v + c;
+      if (total) *total = excl + v + c;
+    }
+  }
+};
 
 // group offsets goff[0..ng] and the stream length at off[nblk]
 struct GroupOffsetSink {
@@ -801,6 +867,68 @@ hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int
   } else {
     zr_emit_kernel<<<zr_grid(nblk), 256, 0, s>>>(src, nblk, stride, B, eob, off, out, capacity);
   }
+  return hipGetLastError();
+}
+
+// Zero-run encode in one call (ivc_zerorun_encode_dev): dense rows through the int8 hand-off are
+// pipelined over K chunks of groups — on the caller's stream chunk j's count pass and its scan
+// (continuing chunk j - 1's total), on the second stream chunk j's emission as soon as its
+// offsets are known, so the memory-bound count pass of chunk j + 1 overlaps the issue-bound
+// emission of chunk j.  Other rows: the two passes in order.
+#ifndef IVC_ZR_CHUNKS
+#define IVC_ZR_CHUNKS 32
+#endif
+hipError_t launch_zerorun_encode(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
+                                 void* scratch, int64_t* off, int32_t* out, int64_t capacity,
+                                 hipStream_t s) {
+  const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
+  int K = IVC_ZR_CHUNKS;
+  if (K > PIPE_EVENTS - 2) K = PIPE_EVENTS - 2;
+  if (ng < 2048 * (int64_t)K) K = 1;
+  const char* f = getenv("IVC_ZR_FORCE_CHUNKS");   // test hook (per call): K chunks, any size
+  if (f && f[0]) K = std::max(1, std::min(atoi(f), PIPE_EVENTS - 2));
+  if (!IVC_ZC || !zw_ok(src, stride, B)) K = 1;
+  if (K <= 1) {
+    hipError_t e = launch_zerorun_offsets(src, nblk, stride, B, scratch, off, s);
+    if (e == hipSuccess) e = launch_zerorun_emit(src, nblk, stride, B, eob, scratch, off, out, capacity, s);
+    return e;
+  }
+  PipeCtx* pp = nullptr;
+  hipError_t e = pipe_ctx(&pp);
+  if (e != hipSuccess) return e;
+  PipeCtx& P = *pp;
+  std::lock_guard<std::mutex> lock(P.mu);
+  const ZrScratch z = zr_scratch(scratch, nblk);
+  if ((e = hipMemsetAsync(z.zc.ctl, 0, 8, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(z.goff, 0, 8, s)) != hipSuccess) return e;
+  if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 2], s)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(P.aux, P.ev[PIPE_EVENTS - 2], 0)) != hipSuccess) return e;
+  // chunks of whole NGR-group batches so no count wave straddles two chunks
+  const int64_t unit = IVC_ZW_COUNT_GROUPS;
+  const int64_t per = ((ng + K - 1) / K + unit - 1) / unit * unit;
+  for (int j = 0; j < K; ++j) {
+    const int64_t g0 = std::min<int64_t>((int64_t)j * per, ng), g1 = std::min<int64_t>(g0 + per, ng);
+    if (g1 <= g0) break;
+    const int64_t len = g1 - g0;
+    zw_count_kernel<true><<<zw_grid((len * ZW_BLK + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(
+        src, nblk, z.counts, z.zc, g0, g1);
+    e = device_scan<int64_t>(len, CountGen{z.counts + g0}, SumI64{},
+                             GroupOffsetCarrySink{z.goff + g0, len, z.goff + g0,
+                                                  g1 == ng ? off + nblk : nullptr},
+                             z.agg, s);
+    if (e != hipSuccess) return e;
+    if ((e = hipEventRecord(P.ev[j], s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(P.aux, P.ev[j], 0)) != hipSuccess) return e;
+    zc_emit_kernel<<<zw_grid(len * ZW_BLK, 6), 256, 0, P.aux>>>(nblk, eob, z.goff, z.zc.c8, z.zc.c16,
+                                                              z.zc.flag, z.zc.ctl + 1, off, out,
+                                                              capacity, g0, g1);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0)) != hipSuccess) return e;
+  // a value outside int16 anywhere (or the int16 slots ran out): every group from the int32 rows
+  zw_emit_kernel<<<zw_grid((nblk + IVC_ZW_EMIT_GROUPS - 1) / IVC_ZW_EMIT_GROUPS, 6), 256, 0, s>>>(
+      src, nblk, eob, z.goff, off, out, capacity, z.zc.ctl + 1);
   return hipGetLastError();
 }
 
@@ -976,50 +1104,58 @@ __device__ __forceinline__ void zf_load_tile(const int32_t* __restrict__ s, int6
     }
   }
 }
+// tiles [t_begin, t_end) (t_end < 0: to the stream's end)
 __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict__ s, int64_t n,
                                                        int32_t eob, int32_t* __restrict__ tile_eobs,
-                                                       int* fail, uint32_t* __restrict__ eobmask) {
+                                                       int* fail, uint32_t* __restrict__ eobmask,
+                                                       int64_t t_begin = 0, int64_t t_end = -1) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t ntiles = (n + ZF_TILE - 1) / ZF_TILE;
+  const int64_t ntiles = t_end < 0 ? (n + ZF_TILE - 1) / ZF_TILE : t_end;
   ZfTile cur;
-  if ((int64_t)blockIdx.x < ntiles) zf_load_tile(s, n, blockIdx.x, w, lane, cur);
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  if (t_begin + (int64_t)blockIdx.x < ntiles) zf_load_tile(s, n, t_begin + blockIdx.x, w, lane, cur);
+  for (int64_t t = t_begin + blockIdx.x; t < ntiles; t += gridDim.x) {
     ZfTile nxt;
     if (t + gridDim.x < ntiles) zf_load_tile(s, n, t + gridDim.x, w, lane, nxt);
     int cnt = 0;
     bool bad = false;
     int last = cur.p0[0];                    // (IVC_ZF_WAVE_CONTIG) the symbol before step k
+    // a tile wholly inside the stream needs no per-symbol bounds test (all but the last)
+    auto count_tile = [&](auto full_c) {
+      constexpr bool FULL = decltype(full_c)::value;
 #pragma unroll
-    for (int k = 0; k < ZF_TILE / 1024; ++k) {
-      const int off = zf_off(w, k, lane);
-      const int64_t i = t * ZF_TILE + off;
-      const int v[4] = {cur.q[k].x, cur.q[k].y, cur.q[k].z, cur.q[k].w};
-      // the symbol before: the previous lane's last (DPP), lane 0's from the scalar load or
-      // the previous step's lane 63
-      const int p0 = IVC_ZF_WAVE_CONTIG ? last : cur.p0[k];
-      int pv = __builtin_amdgcn_update_dpp(p0, v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
-      if (IVC_ZF_WAVE_CONTIG) last = __builtin_amdgcn_readlane(v[3], 63);
-      uint32_t bits = 0;
+      for (int k = 0; k < ZF_TILE / 1024; ++k) {
+        const int off = zf_off(w, k, lane);
+        const int64_t i = t * ZF_TILE + off;
+        const int v[4] = {cur.q[k].x, cur.q[k].y, cur.q[k].z, cur.q[k].w};
+        // the symbol before: the previous lane's last (DPP), lane 0's from the scalar load or
+        // the previous step's lane 63
+        const int p0 = IVC_ZF_WAVE_CONTIG ? last : cur.p0[k];
+        int pv = __builtin_amdgcn_update_dpp(p0, v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
+        if (IVC_ZF_WAVE_CONTIG) last = __builtin_amdgcn_readlane(v[3], 63);
+        uint32_t bits = 0;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (i + e < n) {
-          const bool eb = v[e] == eob && pv != 0;
-          cnt += eb ? 1 : 0;
-          bits |= eb ? 1u << e : 0u;
-          bad |= pv == 0 && v[e] <= 0;
+        for (int e = 0; e < 4; ++e) {
+          if (FULL || i + e < n) {
+            const bool eb = v[e] == eob && pv != 0;
+            bits |= eb ? 1u << e : 0u;
+            bad |= pv == 0 && v[e] <= 0;
+          }
+          pv = v[e];
         }
-        pv = v[e];
+        cnt += __builtin_popcount(bits);
+        if (eobmask) {
+          // 8 lanes' nibbles make one word: OR by DPP (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror)
+          bits <<= 4 * (lane & 7);
+          bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);
+          bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xf, 0xf, false);
+          bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x141, 0xf, 0xf, false);
+          if ((lane & 7) == 0) eobmask[t * (ZF_TILE / 32) + off / 32] = bits;
+        }
       }
-      if (eobmask) {
-        // 8 lanes' nibbles make one word: OR by DPP (quad_perm 1,0,3,2 / 2,3,0,1, row_half_mirror)
-        bits <<= 4 * (lane & 7);
-        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0xB1, 0xf, 0xf, false);
-        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x4E, 0xf, 0xf, false);
-        bits |= (uint32_t)__builtin_amdgcn_mov_dpp((int)bits, 0x141, 0xf, 0xf, false);
-        if ((lane & 7) == 0) eobmask[t * (ZF_TILE / 32) + off / 32] = bits;
-      }
-    }
+    };
+    if ((t + 1) * ZF_TILE <= n) count_tile(std::true_type{});
+    else count_tile(std::false_type{});
     // the wave's count by DPP (no LDS: an LDS wait would also wait for the prefetched scalar load)
     cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x111, 0xf, 0xf, false);   // row_shr:1
     cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x112, 0xf, 0xf, false);   // row_shr:2
@@ -1185,6 +1321,7 @@ __global__ void zr_decode_verdict_gated(const int32_t* s, const uint8_t* is_rl, 
 }
 
 namespace {
+constexpr int S2I_MAX_CHUNKS = 64;
 struct ZrDecScratch {
   uint8_t* is_rl;
   int64_t* agg;
@@ -1197,6 +1334,7 @@ struct ZrDecScratch {
   int* flags;               // [0] fail, [1] ok
   uint32_t* eobmask;        // symbols -> image: ntf * ZF_TILE / 32 words
   int64_t* gstart;          // symbols -> image: ngroups + 1
+  int64_t* grange;          // symbols -> image, pipelined: [S2I_MAX_CHUNKS][2] group ranges
 };
 int64_t align16(int64_t b) { return (b + 15) / 16 * 16; }
 ZrDecScratch zr_dec_scratch(void* scratch, int64_t n, int64_t* bytes, int64_t ngroups = -1) {
@@ -1216,9 +1354,11 @@ ZrDecScratch zr_dec_scratch(void* scratch, int64_t n, int64_t* bytes, int64_t ng
   z.flags = (int*)(b + o); o += 16;
   z.eobmask = nullptr;
   z.gstart = nullptr;
+  z.grange = nullptr;
   if (ngroups >= 0) {
     z.eobmask = (uint32_t*)(b + o); o += align16(ntf * (ZF_TILE / 32) * 4);
     z.gstart = (int64_t*)(b + o); o += align16((ngroups + 1) * 8);
+    z.grange = (int64_t*)(b + o); o += align16(S2I_MAX_CHUNKS * 2 * 8);
   }
   if (bytes) *bytes = o;
   return z;
@@ -1292,13 +1432,12 @@ int64_t sym_image_scratch_bytes(int64_t n, int64_t ngroups) {
   return bytes;
 }
 
-// test hook, read once per process (see launch_symbols2image)
+// test hook (see launch_symbols2image)
 static bool s2i_no_fallback() {
-  static const bool v = [] {
-    const char* nf = getenv("IVC_S2I_NO_FALLBACK");
-    return nf && nf[0] == '1';
-  }();
-  return v;
+  // read per call (a getenv, negligible next to the call): a test can set and clear it
+  // between calls in one process
+  const char* nf = getenv("IVC_S2I_NO_FALLBACK");
+  return nf && nf[0] == '1';
 }
 
 constexpr int64_t IVC_S2I_REJECTED = -100;
@@ -1307,6 +1446,75 @@ __global__ void s2i_rejected_verdict(const int* ok, int64_t* err) {
   err[0] = IVC_S2I_REJECTED;
   err[1] = 0;
   err[2] = 0;
+}
+
+// Pipelined symbols -> image: the stream is cut into K chunks of tiles; on the caller's stream
+// chunk j's EOB count, its tile scan (continuing chunk j - 1's totals) and its group starts
+// run in order, and on a second stream the decode of the groups chunk j - 1 owns starts as soon
+// as chunk j's starts are known (its last group ends in chunk j) — so the stream pass of chunk
+// j + 1 overlaps the decode of chunk j - 1 (the decode leaves VGPRs and wave slots for it).
+#ifndef IVC_S2I_CHUNKS
+#define IVC_S2I_CHUNKS 32
+#endif
+static int s2i_chunks(int64_t ntf) {
+  // test hook (read per call): IVC_S2I_FORCE_CHUNKS=K pipelines any stream of >= K tiles
+  const char* f = getenv("IVC_S2I_FORCE_CHUNKS");
+  if (f && f[0]) {
+    int K = atoi(f);
+    if (K > S2I_MAX_CHUNKS) K = S2I_MAX_CHUNKS;
+    if (ntf < K) K = (int)ntf;
+    return K < 1 ? 1 : K;
+  }
+  int K = IVC_S2I_CHUNKS;
+  if (K > S2I_MAX_CHUNKS) K = S2I_MAX_CHUNKS;
+  if (ntf < 64 * (int64_t)K) K = 1;          // small streams: one pass
+  return K < 1 ? 1 : K;
+}
+
+static hipError_t s2i_pipelined(const int32_t* sym, int64_t n, int32_t eob, int64_t ntf, int K,
+                                int64_t nframes, int64_t H, int64_t W, int C, const QTab& t,
+                                int to_rgb, double* out, const ZrDecScratch& z, hipStream_t s) {
+  PipeCtx* pp = nullptr;
+  hipError_t e = pipe_ctx(&pp);
+  if (e != hipSuccess) return e;
+  PipeCtx& P = *pp;
+  std::lock_guard<std::mutex> lock(P.mu);
+  const int64_t ngroups = nframes * (H / 8) * ((W / 8 + 7) / 8);
+  if ((e = hipMemsetAsync(z.gstart, 0xff, (size_t)(ngroups + 1) * 8, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(z.tile_first, 0, 8, s)) != hipSuccess) return e;
+  if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 2], s)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(P.aux, P.ev[PIPE_EVENTS - 2], 0)) != hipSuccess) return e;
+  const int64_t per = (ntf + K - 1) / K;
+  auto tile0 = [&](int j) { return std::min<int64_t>((int64_t)j * per, ntf); };
+  for (int j = 0; j < K; ++j) {
+    const int64_t a = tile0(j), b = tile0(j + 1);
+    if (b > a) {
+      const int64_t len = b - a;
+      const unsigned grid = (unsigned)(len < 256 * 8 ? len : 256 * 8);
+      zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags, z.eobmask, a, b);
+      e = device_scan<int64_t>(len, CountGen{z.tile_eobs + a}, SumI64{},
+                               OffsetCarrySink{z.tile_first + a, len, z.tile_first + a}, z.fagg, s);
+      if (e == hipSuccess)
+        e = launch_sym_locate_range(z.eobmask, z.tile_first, a, b, nframes, H, W, C, z.gstart, s);
+      if (e != hipSuccess) return e;
+    }
+    // chunk j's group range (its E bounds are final now)
+    if ((e = launch_sym_group_range(z.tile_first, a, b, j == 0, j == K - 1, nframes, H, W, C,
+                                    z.grange + 2 * j, s)) != hipSuccess)
+      return e;
+    if ((e = hipEventRecord(P.ev[j], s)) != hipSuccess) return e;
+    if (j >= 1) {                                  // chunk j - 1's groups end by chunk j's starts
+      if ((e = hipStreamWaitEvent(P.aux, P.ev[j], 0)) != hipSuccess) return e;
+      if ((e = launch_sym_image_range(sym, n, eob, nframes, H, W, C, t, to_rgb, out, z.gstart,
+                                      z.flags, z.grange + 2 * (j - 1), P.aux)) != hipSuccess)
+        return e;
+    }
+  }
+  if ((e = launch_sym_image_range(sym, n, eob, nframes, H, W, C, t, to_rgb, out, z.gstart, z.flags,
+                                  z.grange + 2 * (K - 1), P.aux)) != hipSuccess)
+    return e;
+  if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux)) != hipSuccess) return e;
+  return hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0);
 }
 
 hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, int64_t H,
@@ -1321,16 +1529,22 @@ hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, 
   const int* skip = nullptr;
   if (n > 0 && expected > 0 && eob != 0 && ((uintptr_t)sym & 15) == 0) {
     const int64_t ntf = (n + ZF_TILE - 1) / ZF_TILE;
-    const unsigned grid = (unsigned)(ntf < 256 * 8 ? ntf : 256 * 8);
     if ((e = hipMemsetAsync(z.flags, 0, 16, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(z.tile_eobs, 0, (size_t)ntf * 4, s)) != hipSuccess) return e;
-    zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags, z.eobmask);
-    e = device_scan<int64_t>(ntf, CountGen{z.tile_eobs}, SumI64{}, OffsetSink{z.tile_first, ntf},
-                             z.fagg, s);
-    if (e != hipSuccess) return e;
-    e = launch_sym_image(sym, n, eob, z.eobmask, z.tile_first, ntf, nframes, H, W, C, t, to_rgb,
-                         out, z.gstart, z.flags, s);
-    if (e != hipSuccess) return e;
+    const int K = s2i_chunks(ntf);
+    if (K <= 1) {
+      const unsigned grid = (unsigned)(ntf < 256 * 8 ? ntf : 256 * 8);
+      zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags, z.eobmask);
+      e = device_scan<int64_t>(ntf, CountGen{z.tile_eobs}, SumI64{}, OffsetSink{z.tile_first, ntf},
+                               z.fagg, s);
+      if (e != hipSuccess) return e;
+      e = launch_sym_image(sym, n, eob, z.eobmask, z.tile_first, ntf, nframes, H, W, C, t, to_rgb,
+                           out, z.gstart, z.flags, s);
+      if (e != hipSuccess) return e;
+    } else if ((e = s2i_pipelined(sym, n, eob, ntf, K, nframes, H, W, C, t, to_rgb, out, z, s)) !=
+               hipSuccess) {
+      return e;
+    }
     zf_finish<<<1, 1, 0, s>>>(z.flags, z.tile_first + ntf, expected, z.flags + 1, err);
     skip = z.flags + 1;
   }

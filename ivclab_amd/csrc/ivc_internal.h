@@ -53,6 +53,16 @@ hipError_t launch_sym_image(const int32_t* sym, int64_t n, int32_t eob, const ui
                             const int64_t* tile_first, int64_t ntiles, int64_t nframes, int64_t H,
                             int64_t W, int C, const QTab& t, int to_rgb, double* out,
                             int64_t* gstart, int* fail, hipStream_t s);
+hipError_t launch_sym_locate_range(const uint32_t* eobmask, const int64_t* tile_first, int64_t t0,
+                                   int64_t t1, int64_t nframes, int64_t H, int64_t W, int C,
+                                   int64_t* gstart, hipStream_t s);
+hipError_t launch_sym_group_range(const int64_t* tile_first, int64_t tc0, int64_t tc1, int first,
+                                  int last, int64_t nframes, int64_t H, int64_t W, int C,
+                                  int64_t* range, hipStream_t s);
+hipError_t launch_sym_image_range(const int32_t* sym, int64_t n, int32_t eob, int64_t nframes,
+                                  int64_t H, int64_t W, int C, const QTab& t, int to_rgb,
+                                  double* out, const int64_t* gstart, int* fail,
+                                  const int64_t* grange, hipStream_t s);
 int64_t sym_image_scratch_bytes(int64_t n, int64_t ngroups);
 hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, int64_t H,
                                 int64_t W, int C, const QTab& t, int32_t eob, int to_rgb,
@@ -85,6 +95,10 @@ hipError_t launch_zerorun_offsets(const int32_t* src, int64_t nblk, int stride, 
 hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
                                void* scratch, int64_t* off, int32_t* out, int64_t capacity,
                                hipStream_t s);
+// offsets + emission in one call (pipelined over chunks of groups for dense rows)
+hipError_t launch_zerorun_encode(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
+                                 void* scratch, int64_t* off, int32_t* out, int64_t capacity,
+                                 hipStream_t s);
 int64_t zr_decode_scratch_bytes(int64_t n);
 hipError_t launch_rgb2ycbcr(const void* src, int dtype, int64_t npix, double* dst, hipStream_t s);
 hipError_t launch_ycbcr2rgb(const void* src, int dtype, int64_t npix, int64_t cstride, void* dst,

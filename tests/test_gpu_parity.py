@@ -979,14 +979,18 @@ def test_zerorun_device_wide_and_general(nblk):
     assert torch.equal(off2, off) and np.array_equal(out2.cpu().numpy(), want)
 
 
+@pytest.mark.parametrize("chunks", [None, 5])
 @pytest.mark.parametrize("tier", ["int8", "some_int16", "int32_value", "int16_slots_full"])
-def test_zerorun_int8_handoff_tiers(tier):
+def test_zerorun_int8_handoff_tiers(tier, chunks, monkeypatch):
     """The dense-row encoder hands the coefficients from its count pass to its emission pass
     as int8, a group with a value outside int8 as int16 (side slots for 1 in 8 groups), and
     falls back to emitting from the int32 rows when a value lies outside int16 or the int16
-    slots run out: every tier gives the oracle's stream and offsets."""
+    slots run out: every tier gives the oracle's stream and offsets, in one pass and pipelined
+    over 5 chunks of groups (a later chunk's wide value sends every chunk to the fallback)."""
     torch = pytest.importorskip("torch")
     import ivclab_amd.device as D
+    if chunks:     # the pipelined call (count of chunk j + 1 beside the emission of chunk j)
+        monkeypatch.setenv("IVC_ZR_FORCE_CHUNKS", str(chunks))
     nblk = 16 * 2000 + 3
     rng = np.random.default_rng(hash(tier) % 1000)
     x = rng.integers(-100, 101, (nblk, 64)).astype(np.int32)

@@ -238,8 +238,8 @@ def test_chunked_inter_encode_with_side_stream_histograms():
     assert_bits(q2[3], wq.reshape(H // 8, W // 8, 3, 64), "q pair 3")
 
 
-@pytest.mark.parametrize("C", [3, 1])
-def test_symbols2image_fused_adversarial(monkeypatch, C):
+@pytest.mark.parametrize("C,chunks", [(3, None), (1, None), (3, 3), (1, 16)])
+def test_symbols2image_fused_adversarial(monkeypatch, C, chunks):
     """The fused symbols -> image kernel (ivc_decode.hip sym_image_kernel: zero-run expansion
     into LDS, dequantise, IDCT, unpatch, ycbcr2rgb; intracodec.py:84-146 + zerorun.py:44-88)
     alone — IVC_S2I_NO_FALLBACK=1 keeps the general decoder from overwriting its image — on
@@ -249,6 +249,8 @@ def test_symbols2image_fused_adversarial(monkeypatch, C):
     (w = 125 block columns) and a stream of 130k-380k symbols over 30-90 tiles; against the
     oracle chain (ZeroRunCoder.decode, unflatten, dequantise, IDCT, unpatch, ycbcr2rgb)."""
     monkeypatch.setenv("IVC_S2I_NO_FALLBACK", "1")
+    if chunks:     # the pipelined call (ivc_entropy.hip s2i_pipelined) on a stream of 30-90 tiles
+        monkeypatch.setenv("IVC_S2I_FORCE_CHUNKS", str(chunks))
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(40 + C)
     F, H, W = 2, 128, 1000
@@ -275,3 +277,42 @@ def test_symbols2image_fused_adversarial(monkeypatch, C):
         if C == 3:
             want = O.ycbcr2rgb(want)
         assert_bits(out[f].cpu().numpy(), want, f"fused symbols2image C={C} frame {f}")
+
+
+@pytest.mark.parametrize("chunks", [1, 4, 13])
+def test_symbols2image_pipelined_rejects_and_falls_back(monkeypatch, chunks):
+    """A malformed block (a run past 64 coefficients) in the middle of a 40-tile stream: the
+    fused path — one pass or pipelined over chunks of tiles — rejects the stream
+    (IVC_S2I_NO_FALLBACK reports IVC_S2I_REJECTED), and with the fallback the call reports the
+    reference's error, as ZeroRunCoder.decode raises it (zerorun.py:66-70)."""
+    from ivclab_amd.image import IntraCodec
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(77)
+    F, H, W, C = 1, 128, 1000, 3
+    q = rng.integers(-3, 4, (F, H // 8, W // 8, C, 64)).astype(np.int32)
+    q[..., 8:] *= rng.random(q[..., 8:].shape) < 0.15
+    sym = np.asarray(O.zerorun_encode_fast(q.reshape(-1, 64)), dtype=np.int32)
+    eobs = np.flatnonzero(sym == 4000)
+    cut = eobs[len(eobs) // 2] + 1                     # a block boundary mid-stream
+    bad = np.concatenate([sym[:cut], [0, 70], sym[cut:]]).astype(np.int32)
+    table = PatchQuant(1.0).get_quantization_table()
+    monkeypatch.setenv("IVC_S2I_FORCE_CHUNKS", str(chunks))
+    out = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
+    err = torch.full((3,), -1, dtype=torch.int64, device=dev)
+    # the clean stream decodes identically whatever the chunking
+    D.symbols2image(torch.from_numpy(sym).to(dev), C, table, out, err, to_rgb=True)
+    torch.cuda.synchronize()
+    assert err.tolist() == [0, 0, 0]
+    want0 = O.ycbcr2rgb(O.unpatch(O.intra_decode(q[0], 1.0, unzigzag=True)))
+    assert_bits(out[0].cpu().numpy(), want0, f"clean stream, chunks={chunks}")
+    monkeypatch.setenv("IVC_S2I_NO_FALLBACK", "1")
+    D.symbols2image(torch.from_numpy(bad).to(dev), C, table, out, err, to_rgb=True)
+    torch.cuda.synchronize()
+    assert int(err[0]) == -100, err.tolist()
+    monkeypatch.delenv("IVC_S2I_NO_FALLBACK")
+    codec = IntraCodec(quantization_scale=1.0)
+    with pytest.raises(Exception) as got:
+        codec.symbols2image(bad, (H, W, 3))
+    with pytest.raises(Exception) as want:
+        O.zerorun_decode(list(bad), (H // 8, W // 8, C))
+    assert type(got.value) is type(want.value) and str(got.value) == str(want.value)
