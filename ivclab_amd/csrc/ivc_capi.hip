@@ -1019,6 +1019,50 @@ int ivc_motion_compensate(const void* ref, int esize, int64_t nframes, int64_t H
 }
 
 // ---------------------------------------------------------------- fused inter ---------
+// ME then the residual encoder.  Long sequences are pipelined over K chunks of frame pairs: the
+// search of chunk j + 1 on the caller's stream beside the residual encode of chunk j on the
+// second stream (ME is latency-bound, the residual encoder HBM-bound).
+#ifndef IVC_INTER_CHUNKS
+#define IVC_INTER_CHUNKS 1
+#endif
+static int inter_encode_enqueue(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W, int sr,
+                                const QTab& t, int zigzag, int64_t* mv, int32_t* out, int64_t* hist,
+                                int32_t hist_lo, int32_t hist_n, hipStream_t s) {
+  const int64_t HW = H * W, npairs = nframes - 1, hw = (H / 8) * (W / 8);
+  int K = IVC_INTER_CHUNKS;
+  if (const char* f = getenv("IVC_INTER_FORCE_CHUNKS")) K = atoi(f);   // test hook, per call
+  if (K > PIPE_EVENTS - 2) K = PIPE_EVENTS - 2;
+  if (K > npairs) K = (int)npairs;
+  auto residual = [&](int64_t p0, int64_t p1, hipStream_t st) {
+    return launch_inter_residual(frames + p0 * HW, p1 - p0, H, W, sr, mv + p0 * hw, t, zigzag,
+                                 out + p0 * hw * 192, st, hist, hist_lo, hist_n);
+  };
+  if (K <= 1) {
+    TRY(dev_launch(launch_motion_estimate(frames, frames + HW, IVC_U8, npairs, H, W, sr,
+                                          IVC_ME_EXACT_U8, mv, s), "motion_estimate"));
+    return dev_launch(residual(0, npairs, s), "inter_residual");
+  }
+  PipeCtx* pp = nullptr;
+  TRY(dev_launch(pipe_ctx(&pp), "inter_encode"));
+  PipeCtx& P = *pp;
+  std::lock_guard<std::mutex> lock(P.mu);
+  TRY(dev_launch(hipEventRecord(P.ev[PIPE_EVENTS - 2], s), "inter_encode"));
+  TRY(dev_launch(hipStreamWaitEvent(P.aux, P.ev[PIPE_EVENTS - 2], 0), "inter_encode"));
+  const int64_t per = (npairs + K - 1) / K;
+  for (int j = 0; j < K; ++j) {
+    const int64_t p0 = std::min<int64_t>((int64_t)j * per, npairs), p1 = std::min<int64_t>(p0 + per, npairs);
+    if (p1 <= p0) break;
+    TRY(dev_launch(launch_motion_estimate(frames + p0 * HW, frames + (p0 + 1) * HW, IVC_U8, p1 - p0,
+                                          H, W, sr, IVC_ME_EXACT_U8, mv + p0 * hw, s),
+                   "motion_estimate"));
+    TRY(dev_launch(hipEventRecord(P.ev[j], s), "inter_encode"));
+    TRY(dev_launch(hipStreamWaitEvent(P.aux, P.ev[j], 0), "inter_encode"));
+    TRY(dev_launch(residual(p0, p1, P.aux), "inter_residual"));
+  }
+  TRY(dev_launch(hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux), "inter_encode"));
+  return dev_launch(hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0), "inter_encode");
+}
+
 int ivc_inter_encode_dev(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W, int sr,
                          const double* table, int calc_dtype, int zigzag, int64_t* mv,
                          int32_t* out, void* stream) {
@@ -1030,12 +1074,8 @@ int ivc_inter_encode_dev(const uint8_t* frames, int64_t nframes, int64_t H, int6
   if (nframes < 2) return IVC_OK;
   QTab t;
   TRY(load_table(table, &t));
-  hipStream_t s = (hipStream_t)stream;
-  const int64_t HW = H * W;
-  TRY(dev_launch(launch_motion_estimate(frames, frames + HW, IVC_U8, nframes - 1, H, W, sr,
-                                        IVC_ME_EXACT_U8, mv, s), "motion_estimate"));
-  return dev_launch(launch_inter_residual(frames, nframes - 1, H, W, sr, mv, t, zigzag, out, s),
-                    "inter_residual");
+  return inter_encode_enqueue(frames, nframes, H, W, sr, t, zigzag, mv, out, nullptr, 0, 0,
+                              (hipStream_t)stream);
 }
 
 int ivc_inter_encode_hist_dev(const uint8_t* frames, int64_t nframes, int64_t H, int64_t W, int sr,
@@ -1051,12 +1091,8 @@ int ivc_inter_encode_hist_dev(const uint8_t* frames, int64_t nframes, int64_t H,
   if (nframes < 2) return IVC_OK;
   QTab t;
   TRY(load_table(table, &t));
-  hipStream_t s = (hipStream_t)stream;
-  const int64_t HW = H * W;
-  TRY(dev_launch(launch_motion_estimate(frames, frames + HW, IVC_U8, nframes - 1, H, W, sr,
-                                        IVC_ME_EXACT_U8, mv, s), "motion_estimate"));
-  return dev_launch(launch_inter_residual(frames, nframes - 1, H, W, sr, mv, t, zigzag, out, s,
-                                          hist, hist_lo, hist_n), "inter_residual");
+  return inter_encode_enqueue(frames, nframes, H, W, sr, t, zigzag, mv, out, hist, hist_lo, hist_n,
+                              (hipStream_t)stream);
 }
 
 // ---------------------------------------------------------------- histogram -----------

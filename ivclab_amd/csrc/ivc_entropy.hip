@@ -26,18 +26,11 @@
 namespace ivc {
 
 // A second stream (and events) per device for the pipelined calls (symbols2image, zero-run
-// encode): work on it is ordered against the caller's stream by events; the mutex serialises
-// the enqueue of concurrent host threads.
-constexpr int PIPE_EVENTS = 66;
-struct PipeCtx {
-  hipStream_t aux = nullptr;
-  hipEvent_t ev[PIPE_EVENTS] = {};
-  std::mutex mu;
-  bool ok = false;
-};
+// encode, inter encode; PipeCtx in ivc_internal.h): work on it is ordered against the caller's
+// stream by events; the mutex serialises the enqueue of concurrent host threads.
 static PipeCtx g_pipe[64];
 static std::once_flag g_pipe_once[64];
-static hipError_t pipe_ctx(PipeCtx** out) {
+hipError_t pipe_ctx(PipeCtx** out) {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;

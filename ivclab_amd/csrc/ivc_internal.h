@@ -1,12 +1,24 @@
 // ivc_internal.h — launchers shared between the kernels (ivc_kernels.hip, ivc_motion.hip)
 // and the C-ABI layer (ivc_capi.hip).  Not part of the public interface (include/ivc.h).
 #pragma once
+#include <mutex>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "../../include/ivc.h"
 
 namespace ivc {
+
+// the per-device second stream of the pipelined calls (ivc_entropy.hip)
+constexpr int PIPE_EVENTS = 66;
+struct PipeCtx {
+  hipStream_t aux = nullptr;
+  hipEvent_t ev[PIPE_EVENTS] = {};
+  std::mutex mu;
+  bool ok = false;
+};
+hipError_t pipe_ctx(PipeCtx** out);
+
 
 // quantisation table as kernel argument (by value: no per-call upload on the stream)
 //   q[p*64 + i*8 + k]  : table value in the calc dtype (exactly representable)
