@@ -630,6 +630,8 @@ hipError_t launch_sym_image_range(const int32_t* sym, int64_t n, int32_t eob, in
   const DecArgs a = s2i_args(nframes, H, W, out);
   SymImageArgs z{sym, n, eob, gstart, fail};
   auto go = [&](auto k) {
+    // (a chunk's launch keeps the whole resident grid: 3/4 or 7/8 of it, leaving room for the
+    // next chunk's EOB pass, measured 9-10 % slower)
     const unsigned grid = resident_grid_ptr(reinterpret_cast<const void*>(k), (a.ngroups + 3) / 4);
     k<<<grid, 256, 0, s>>>(a, z, t, grange);
   };
