@@ -1048,6 +1048,7 @@ static int inter_encode_enqueue(const uint8_t* frames, int64_t nframes, int64_t 
   std::lock_guard<std::mutex> lock(P.mu);
   TRY(dev_launch(hipEventRecord(P.ev[PIPE_EVENTS - 2], s), "inter_encode"));
   TRY(dev_launch(hipStreamWaitEvent(P.aux, P.ev[PIPE_EVENTS - 2], 0), "inter_encode"));
+  PipeJoin join{P, s, true};
   const int64_t per = (npairs + K - 1) / K;
   for (int j = 0; j < K; ++j) {
     const int64_t p0 = std::min<int64_t>((int64_t)j * per, npairs), p1 = std::min<int64_t>(p0 + per, npairs);
@@ -1059,6 +1060,7 @@ static int inter_encode_enqueue(const uint8_t* frames, int64_t nframes, int64_t 
     TRY(dev_launch(hipStreamWaitEvent(P.aux, P.ev[j], 0), "inter_encode"));
     TRY(dev_launch(residual(p0, p1, P.aux), "inter_residual"));
   }
+  join.armed = false;
   TRY(dev_launch(hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux), "inter_encode"));
   return dev_launch(hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0), "inter_encode");
 }

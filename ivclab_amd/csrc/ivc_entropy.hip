@@ -28,6 +28,9 @@ namespace ivc {
 // A second stream (and events) per device for the pipelined calls (symbols2image, zero-run
 // encode, inter encode; PipeCtx in ivc_internal.h): work on it is ordered against the caller's
 // stream by events; the mutex serialises the enqueue of concurrent host threads.
+#ifndef IVC_PIPE_PRIORITY
+#define IVC_PIPE_PRIORITY 1
+#endif
 static PipeCtx g_pipe[64];
 static std::once_flag g_pipe_once[64];
 hipError_t pipe_ctx(PipeCtx** out) {
@@ -37,7 +40,16 @@ hipError_t pipe_ctx(PipeCtx** out) {
   if (dev < 0 || dev >= 64) return hipErrorInvalidDevice;
   PipeCtx& P = g_pipe[dev];
   std::call_once(g_pipe_once[dev], [&P] {
-    bool good = hipStreamCreateWithFlags(&P.aux, hipStreamNonBlocking) == hipSuccess;
+    bool good;
+    if (IVC_PIPE_PRIORITY) {
+      // the highest priority: a queue of its own rather than one shared with the caller's
+      // stream when the process has more streams than hardware queues (GPU_MAX_HW_QUEUES)
+      int lo = 0, hi = 0;
+      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+      good = hipStreamCreateWithPriority(&P.aux, hipStreamNonBlocking, hi) == hipSuccess;
+    } else {
+      good = hipStreamCreateWithFlags(&P.aux, hipStreamNonBlocking) == hipSuccess;
+    }
     for (auto& ev : P.ev)
       good = good && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess;
     P.ok = good;
@@ -896,6 +908,7 @@ hipError_t launch_zerorun_encode(const int32_t* src, int64_t nblk, int stride, i
   if ((e = hipMemsetAsync(z.goff, 0, 8, s)) != hipSuccess) return e;
   if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 2], s)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(P.aux, P.ev[PIPE_EVENTS - 2], 0)) != hipSuccess) return e;
+  PipeJoin join{P, s, true};
   // chunks of whole NGR-group batches so no count wave straddles two chunks
   const int64_t unit = IVC_ZW_COUNT_GROUPS;
   const int64_t per = ((ng + K - 1) / K + unit - 1) / unit * unit;
@@ -917,6 +930,7 @@ hipError_t launch_zerorun_encode(const int32_t* src, int64_t nblk, int stride, i
                                                               capacity, g0, g1);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
+  join.armed = false;
   if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0)) != hipSuccess) return e;
   // a value outside int16 anywhere (or the int16 slots ran out): every group from the int32 rows
@@ -1477,6 +1491,7 @@ static hipError_t s2i_pipelined(const int32_t* sym, int64_t n, int32_t eob, int6
   if ((e = hipMemsetAsync(z.tile_first, 0, 8, s)) != hipSuccess) return e;
   if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 2], s)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(P.aux, P.ev[PIPE_EVENTS - 2], 0)) != hipSuccess) return e;
+  PipeJoin join{P, s, true};
   const int64_t per = (ntf + K - 1) / K;
   auto tile0 = [&](int j) { return std::min<int64_t>((int64_t)j * per, ntf); };
   for (int j = 0; j < K; ++j) {
@@ -1506,6 +1521,7 @@ static hipError_t s2i_pipelined(const int32_t* sym, int64_t n, int32_t eob, int6
   if ((e = launch_sym_image_range(sym, n, eob, nframes, H, W, C, t, to_rgb, out, z.gstart, z.flags,
                                   z.grange + 2 * (K - 1), P.aux)) != hipSuccess)
     return e;
+  join.armed = false;
   if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux)) != hipSuccess) return e;
   return hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0);
 }

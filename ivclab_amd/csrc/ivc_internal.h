@@ -18,6 +18,18 @@ struct PipeCtx {
   bool ok = false;
 };
 hipError_t pipe_ctx(PipeCtx** out);
+// Joins the second stream back into the caller's stream when a pipelined enqueue leaves early
+// (an error after work was queued on it): the caller's later frees then wait for that work.
+struct PipeJoin {
+  PipeCtx& P;
+  hipStream_t s;
+  bool armed = false;
+  ~PipeJoin() {
+    if (!armed) return;
+    (void)hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux);
+    (void)hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0);
+  }
+};
 
 
 // quantisation table as kernel argument (by value: no per-call upload on the stream)

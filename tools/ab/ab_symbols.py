@@ -21,7 +21,17 @@ ap.add_argument("libs", nargs="+")
 ap.add_argument("--frames", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--legs", default="", help="comma-separated subset of the legs")
+ap.add_argument("--rccl", action="store_true",
+                help="first create a one-rank RCCL process group (its streams take hardware queues, "
+                     "as in bench.py --rccl)")
 args = ap.parse_args()
+if args.rccl:
+    torch.cuda.set_device(0)
+    from ivclab_amd.distributed import init_single_rank, global_histogram
+    init_single_rank("cuda:0")
+    _h = torch.zeros(8, dtype=torch.int64, device="cuda:0")
+    global_histogram(_h, force=True)          # the communicator and its streams exist now
+    torch.cuda.synchronize()
 N.load_library()
 libs = []
 for p in args.libs:
