@@ -50,10 +50,6 @@ constexpr int DX_WAVE = 8 * 72;  // doubles per wave: transpose image [b][k pitc
 #ifndef IVC_DEC_STORE_AUX
 #define IVC_DEC_STORE_AUX 2      // nt: streamed output
 #endif
-// (A/B) the parse with 4 symbols per lane
-#ifndef IVC_DEC_PARSE4
-#define IVC_DEC_PARSE4 1
-#endif
 // ablation builds only (tools/ab), bits: 1 = the image stores skipped (behind a runtime test the
 // compiler cannot fold), 2 = sym_image_kernel's parse skipped (the staging stays zero)
 #ifndef IVC_DEC_ABLATE
@@ -378,7 +374,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
       }
       __builtin_amdgcn_wave_barrier();
       const int rlen = len - s0 < SYM_SEG ? len - s0 : SYM_SEG;
-#if IVC_DEC_PARSE4
       // 4 symbols per lane (lane l: symbols 4l .. 4l + 3 of a 256-symbol chunk): one wave scan
       // and one LDS round trip per 256 symbols.  A run length is clamped to 127 (anything past
       // 64 already makes its block-plane fail the offset checks), so a chunk's coefficient
@@ -431,37 +426,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
         pcarry += tot & 0xffff;
         bpcarry += tot >> 16;
       }
-#else
-      for (int c0 = 0; c0 < rlen; c0 += 64) {
-        const int i = c0 + lane;
-        const int cur = st[i], prv = st[i - 1], nx = st[i + 1];
-        const bool valid = i < rlen;
-        const bool rl = prv == 0;                      // a run-length slot
-        const bool eobf = valid && !rl && cur == z.eob;
-        const bool isval = valid && !rl && !eobf;
-        const int run = nx < 1 ? 1 : (nx > 4095 ? 4095 : nx);
-        const int cc = isval ? (cur == 0 ? run : 1) : 0;
-        const int packed = (eobf ? (1 << 20) : 0) | cc;
-        const int incl = dec_wave_incl_sum(packed);
-        const int excl = incl - packed;
-        const int pex = pcarry + (excl & 0xfffff);     // this slot's coefficient offset
-        const int bp = bpcarry + (excl >> 20);          // its block-plane
-        // block-plane starts through LDS: an EOB lane records where the next block-plane
-        // starts, then every lane reads its own block-plane's start (in-order LDS per wave)
-        const bool bpok = bp < nbp;
-        if (eobf && bpok) bps[bp + 1] = pex;
-        __builtin_amdgcn_wave_barrier();
-        const int off = pex - bps[bpok ? bp : 0];        // offset inside the block-plane
-        if (isval && cur != 0) {
-          if (off < 64 && bpok && cur == (int)(int16_t)cur) qs[bp * SYM_QP + off] = (int16_t)cur;
-          else bad = true;
-        }
-        if (eobf && (off > 64 || !bpok)) bad = true;
-        const int tot = __builtin_amdgcn_readlane(incl, 63);
-        pcarry += tot & 0xfffff;
-        bpcarry += tot >> 20;
-      }
-#endif
       prevc = st[SYM_SEG - 1];
     }
     if (bpcarry != nbp) bad = true;

@@ -1077,15 +1077,9 @@ constexpr int ZF_TILE = 4096, ZF_HALO = 128;
 // the symbols -> image path locates its groups from it)
 // The next tile's loads are issued before this tile is counted (a wave has 8 KB of reads in
 // flight instead of 4: one load latency per tile measured 3.3 ms for the cfg3 stream, 4.3 TB/s).
-#ifndef IVC_ZF_WAVE_CONTIG
-#define IVC_ZF_WAVE_CONTIG 0
-#endif
-// symbol offset inside the tile of lane `lane` of wave w at step k: IVC_ZF_WAVE_CONTIG gives
-// each wave a contiguous quarter of the tile (the symbol before a lane-0 quad at k > 0 is then
-// lane 63's last of step k - 1, taken by readlane; one scalar load per tile instead of 4)
-__device__ __forceinline__ int zf_off(int w, int k, int lane) {
-  return IVC_ZF_WAVE_CONTIG ? w * (ZF_TILE / 4) + k * 256 + lane * 4 : (k * 256 + w * 64 + lane) * 4;
-}
+// symbol offset inside the tile of lane `lane` of wave w at step k (a wave-contiguous quarter
+// per wave, the predecessor of a lane-0 quad from lane 63's previous step, measured the same)
+__device__ __forceinline__ int zf_off(int w, int k, int lane) { return (k * 256 + w * 64 + lane) * 4; }
 struct ZfTile {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
   i32x4 q[ZF_TILE / 1024];
@@ -1105,7 +1099,7 @@ __device__ __forceinline__ void zf_load_tile(const int32_t* __restrict__ s, int6
     // the symbol before the wave's first: one scalar load per wave (a wave-uniform address),
     // issued with the quads — not a per-lane load (one dword load per lane doubled the vector
     // memory instructions), nor a lane-0 vector load after the quad (a second latency)
-    if (!IVC_ZF_WAVE_CONTIG || k == 0) {
+    {
       const int64_t iw = t * ZF_TILE + zf_off(w, k, 0);
       T.p0[k] = iw > 0 && iw <= n ? s[iw - 1] : 1;   // the stream's first slot is a value slot
     }
@@ -1126,7 +1120,6 @@ __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict
     if (t + gridDim.x < ntiles) zf_load_tile(s, n, t + gridDim.x, w, lane, nxt);
     int cnt = 0;
     bool bad = false;
-    int last = cur.p0[0];                    // (IVC_ZF_WAVE_CONTIG) the symbol before step k
     // a tile wholly inside the stream needs no per-symbol bounds test (all but the last)
     auto count_tile = [&](auto full_c) {
       constexpr bool FULL = decltype(full_c)::value;
@@ -1135,11 +1128,8 @@ __global__ __launch_bounds__(256) void zf_count_kernel(const int32_t* __restrict
         const int off = zf_off(w, k, lane);
         const int64_t i = t * ZF_TILE + off;
         const int v[4] = {cur.q[k].x, cur.q[k].y, cur.q[k].z, cur.q[k].w};
-        // the symbol before: the previous lane's last (DPP), lane 0's from the scalar load or
-        // the previous step's lane 63
-        const int p0 = IVC_ZF_WAVE_CONTIG ? last : cur.p0[k];
-        int pv = __builtin_amdgcn_update_dpp(p0, v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
-        if (IVC_ZF_WAVE_CONTIG) last = __builtin_amdgcn_readlane(v[3], 63);
+        // the symbol before: the previous lane's last (DPP), lane 0's from the scalar load
+        int pv = __builtin_amdgcn_update_dpp(cur.p0[k], v[3], 0x138, 0xf, 0xf, false);   // wave_shr:1
         uint32_t bits = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {

@@ -920,12 +920,6 @@ __device__ __forceinline__ uint32_t zh_bin(const FusedArgs& a, int32_t v, int la
 // m >> lane != 0), their ballot feeds the lane's slot (two mbcnt) — so the scalar unit keeps
 // only the two popcounts and the running fill per block-plane, and no block has a window
 // check (one basic block for the group).  Same slots and values as the general path below.
-#ifndef IVC_EMIT_FLUSH4
-#define IVC_EMIT_FLUSH4 0
-#endif
-#ifndef IVC_EMIT_SLOT_CHAIN
-#define IVC_EMIT_SLOT_CHAIN 1
-#endif
 // a lane's emission slot: base + (bits of m below the lane) + 2 (bits of st below the lane)
 __device__ __forceinline__ int emit_slot(uint64_t m, uint64_t st, int base) {
   uint32_t t = __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)base);
@@ -935,12 +929,6 @@ __device__ __forceinline__ int emit_slot(uint64_t m, uint64_t st, int base) {
   t = __builtin_amdgcn_mbcnt_lo((uint32_t)st, t);
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), t);
 }
-#ifndef IVC_EMIT_TRASH_LATE
-#define IVC_EMIT_TRASH_LATE 0
-#endif
-#ifndef IVC_EMIT_FLUSH_SPLIT
-#define IVC_EMIT_FLUSH_SPLIT 1
-#endif
 template <int C, bool DUP, bool HIST>
 __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* os, int64_t gbase,
                                                   int gcount, const int32_t (&xv)[8][(C == 1 && DUP) ? 2 : 3],
@@ -974,25 +962,16 @@ __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* o
       const uint64_t st = __ballot(rs);
 #endif
       const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
-#if IVC_EMIT_SLOT_CHAIN
       // the lane's slot, fill included: mbcnt accumulates, so m's bits below the lane and st's
       // twice chain into one value (no shifts or adds)
       const int slot = emit_slot(m, st, fill);
-#else
-      const int pos = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) +
-                      2 * (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u));
-#endif
       // a nonzero, a run's 0 + its length, or (the first zero after the last nonzero) the EOB
       const bool w1 = nz || pnz;
       const int32_t v1 = nz || hl ? x : eob;
       const int32_t v2 = rs ? (int32_t)__builtin_ctzll(later) : eob;
 #pragma unroll
       for (int k = 0; k < (p == 1 ? R1 : 1); ++k) {
-#if IVC_EMIT_SLOT_CHAIN
         int32_t* const d = w1 ? zs + slot + (k ? cnt : 0) : zs + ZR_WIN - 65 + lane;
-#else
-        int32_t* const d = w1 ? zs + fill + pos : zs + ZR_WIN - 65 + lane;
-#endif
         d[1] = v2;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // keep the two writes ordered
         d[0] = v1;
@@ -1008,61 +987,10 @@ __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* o
   const int nst = (int)(lim < (int64_t)fill ? (lim > 0 ? lim : 0) : (int64_t)fill);
   const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc(
       a.zr_out + (nst > 0 ? gbase : 0), 0, 4 * nst, 0x00020000);
-#if IVC_EMIT_FLUSH4
-  // 4 symbols per lane: 16-byte LDS reads and stores of whole quads (a quad reaching past the
-  // stored range goes word by word: the buffer range check is not per word)
-  typedef int fq_i32x4 __attribute__((ext_vector_type(4)));
-  for (int j0 = 0; j0 < fill; j0 += 256) {
-    const int j = j0 + 4 * lane;
-    const fq_i32x4 v = *reinterpret_cast<const fq_i32x4*>(zs + j);
-    if (j + 4 <= nst) {
-      __builtin_amdgcn_raw_buffer_store_b128(v, ro, 4 * j, 0, 0);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) __builtin_amdgcn_raw_buffer_store_b32(v[e], ro, 4 * (j + e), 0, 0);
-    }
-    if constexpr (HIST) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool in = j + e < fill;
-        const uint32_t kb = zh_bin(a, v[e], lane);
-        atomicAdd(H.bins + kb, in ? 1u : 0u);
-        if (__builtin_expect(__ballot(in && kb == (uint32_t)ZH_TRASH) != 0, 0)) {
-          if (in && kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v[e], 1u);
-        }
-      }
-    }
-  }
-#elif IVC_EMIT_TRASH_LATE
-  // symbols outside the LDS bins (rare) are remembered per lane and added to the global
-  // histogram in a second walk over the still-intact window: no ballot and branch per 64
-  uint32_t trash = 0;
-  for (int j0 = 0; j0 < fill; j0 += 64) {
-    const int j = j0 + lane;
-    const int32_t v = zs[j];
-    __builtin_amdgcn_raw_buffer_store_b32(v, ro, 4 * j, 0, 0);
-    if constexpr (HIST) {
-      const uint32_t w = j < fill ? 1u : 0u;
-      const uint32_t kb = zh_bin(a, v, lane);
-      atomicAdd(H.bins + kb, w);
-      trash |= kb == (uint32_t)ZH_TRASH ? w : 0u;             // (VALU: no mask merging)
-    }
-  }
-  if constexpr (HIST) {
-    if (__builtin_expect(__ballot(trash != 0u) != 0, 0)) {
-      for (int j0 = 0; j0 < fill; j0 += 64) {
-        const int j = j0 + lane;
-        const int32_t v = zs[j];
-        if (j < fill && zh_bin(a, v, lane) == (uint32_t)ZH_TRASH) zr_hist_global(a, v, 1u);
-      }
-    }
-  }
-#elif IVC_EMIT_FLUSH_SPLIT
   // whole 64-symbol rows without the weight test, then the partial row (the row offset stays
   // in the vector offset: the buffer range check that clips at the caller's capacity does not
   // include the scalar offset)
   const int nfull = fill >> 6;
-#pragma unroll 4
   for (int r = 0; r < nfull; ++r) {
     const int32_t v = zs[64 * r + lane];
     __builtin_amdgcn_raw_buffer_store_b32(v, ro, 4 * (64 * r + lane), 0, 0);
@@ -1086,21 +1014,6 @@ __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* o
       }
     }
   }
-#else
-  for (int j0 = 0; j0 < fill; j0 += 64) {
-    const int j = j0 + lane;
-    const int32_t v = zs[j];
-    __builtin_amdgcn_raw_buffer_store_b32(v, ro, 4 * j, 0, 0);
-    if constexpr (HIST) {
-      const bool in = j < fill;
-      const uint32_t kb = zh_bin(a, v, lane);
-      atomicAdd(H.bins + kb, in ? 1u : 0u);
-      if (__builtin_expect(__ballot(in && kb == (uint32_t)ZH_TRASH) != 0, 0)) {
-        if (in && kb == (uint32_t)ZH_TRASH) zr_hist_global(a, v, 1u);
-      }
-    }
-  }
-#endif
   __builtin_amdgcn_wave_barrier();
 }
 
