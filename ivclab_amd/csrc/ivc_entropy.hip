@@ -419,11 +419,8 @@ __device__ __forceinline__ zv4 zw_load(const int32_t* src, int64_t nblk, int64_t
 #ifndef IVC_ZC_NT
 #define IVC_ZC_NT 1
 #endif
-#ifndef IVC_ZC_EXEC
-#define IVC_ZC_EXEC 1   // exec-masked emission writes (0: dummy words for the idle lanes)
-#endif
 constexpr int ZC_BLK = 16;
-constexpr int ZC_WIN = 1664;   // words per wave: the group's <= 16 x 97 symbols + 65 dummy words
+constexpr int ZC_WIN = 1664;   // words per wave: the group's <= 16 x 97 symbols, padded
 
 struct ZcScratch {
   uint8_t* c8;       // [ng][64 lanes][16 B], byte 4u + e = coefficient 4i + e of block 4u + q
@@ -712,19 +709,11 @@ __global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
       slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), slot);
       const bool w1 = nz || pnz;
       const int32_t v1 = nz || hl ? x : eob;
-#if IVC_ZC_EXEC
       // only the lanes with something to write touch LDS (exec-masked, so the idle lanes' words
       // no longer share banks with the block's slots): a value, a run's 0 or the EOB at the
       // slot; a run's length after it, or the EOB after a nonzero lane 63
       if (w1) os[slot] = v1;
       if (rs || (nz && lane == 63)) os[slot + 1] = rs ? (int32_t)__builtin_ctzll(later) : eob;
-#else
-      const int32_t v2 = rs ? (int32_t)__builtin_ctzll(later) : eob;
-      int32_t* const d = w1 ? os + slot : os + ZC_WIN - 65 + lane;
-      d[1] = v2;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // keep the two writes ordered
-      d[0] = v1;
-#endif
       offv = lane == b ? fill : offv;
       fill += cnt;
       }
