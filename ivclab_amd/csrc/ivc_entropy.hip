@@ -855,6 +855,15 @@ hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* 
   return device_scan<int64_t>(n, CountGen{counts}, SumI64{}, OffsetSink{off, n}, agg, s);
 }
 
+// off[0..n] = off[0] + exclusive int64 prefix of counts[0..n): a chunk of a longer scan whose
+// earlier chunks left their total at off[0] (the pipelined pixels -> symbols call)
+hipError_t launch_exclusive_scan_i32_carry(const int32_t* counts, int64_t n, int64_t* agg,
+                                           int64_t* off, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  return device_scan<int64_t>(n, CountGen{counts}, SumI64{},
+                              GroupOffsetCarrySink{off, n, off, nullptr}, agg, s);
+}
+
 // symbols of every block at its offset; symbols at or past `capacity` are not written.
 // `scratch` is launch_zerorun_offsets' (same src/nblk).
 hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,

@@ -109,6 +109,8 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t s);
 int64_t scan_scratch_elems(int64_t n);
 hipError_t launch_exclusive_scan_i32(const int32_t* counts, int64_t n, int64_t* agg, int64_t* off,
                                      hipStream_t s);
+hipError_t launch_exclusive_scan_i32_carry(const int32_t* counts, int64_t n, int64_t* agg,
+                                           int64_t* off, hipStream_t s);
 hipError_t launch_intra_symbols(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                                 int C, const QTab& t, int32_t eob, int32_t* out, int64_t capacity,
                                 int64_t* nsym, hipStream_t s, int64_t* hist = nullptr,

@@ -2082,6 +2082,69 @@ static void launch_fused_zr(const FusedArgs& a_in, const QTab& t, hipStream_t s)
   k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
 }
 
+// The count pass and the emitter pipelined over K chunks of whole frames (like the zero-run
+// encode, ivc_entropy.hip): chunk j's count pass and its scan (continuing chunk j - 1's total)
+// on the caller's stream, chunk j's emission on the second stream once its offsets exist.  A
+// chunk's groups are contiguous (frame-major group numbering), so every per-group array is
+// addressed from the chunk's first group; chunks start on whole block rows, so the emitter's
+// column bookkeeping is unchanged.
+#ifndef IVC_SYM_CHUNKS
+#define IVC_SYM_CHUNKS 16
+#endif
+static int sym_chunks(int64_t nframes, int64_t ngroups, int64_t gpf) {
+  int K = IVC_SYM_CHUNKS;
+  if (K > PIPE_EVENTS - 2) K = PIPE_EVENTS - 2;
+  if (ngroups < 2048 * (int64_t)K) K = 1;
+  const char* f = getenv("IVC_SYM_FORCE_CHUNKS");   // test hook (per call): K chunks, any size
+  if (f && f[0]) K = std::max(1, std::min(atoi(f), PIPE_EVENTS - 2));
+  if (K > nframes) K = (int)nframes;
+  if (gpf % 4 != 0) K = 1;                           // the emitter reads the flags 4 at a time
+  return K;
+}
+
+template <int C, bool DUP, int NG, typename CountFn>
+static hipError_t intra_symbols_pipelined(const FusedArgs& a, int64_t gpf, int K, int64_t* agg,
+                                          CountFn count, hipStream_t s) {
+  constexpr int NP = (C == 1 && DUP) ? 2 : 3;
+  constexpr int S8 = c8_stride(NP);
+  PipeCtx* pp = nullptr;
+  hipError_t e = pipe_ctx(&pp);
+  if (e != hipSuccess) return e;
+  PipeCtx& P = *pp;
+  std::lock_guard<std::mutex> lock(P.mu);
+  int64_t* off = const_cast<int64_t*>(a.zr_off);
+  if ((e = hipMemsetAsync(off, 0, 8, s)) != hipSuccess) return e;
+  if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 2], s)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(P.aux, P.ev[PIPE_EVENTS - 2], 0)) != hipSuccess) return e;
+  PipeJoin join{P, s, true};
+  const int64_t fpc = ((int64_t)a.nframes + K - 1) / K;
+  const size_t fbytes = (size_t)a.H * a.W * C;          // u8 frames
+  auto k = a.zr_hist ? sym_emit_kernel<C, DUP, true, NG> : sym_emit_kernel<C, DUP, false, NG>;
+  for (int j = 0; j < K; ++j) {
+    const int64_t f0 = (int64_t)j * fpc, f1 = std::min<int64_t>(f0 + fpc, a.nframes);
+    if (f1 <= f0) break;
+    const int64_t g0 = f0 * gpf, len = (f1 - f0) * gpf;
+    FusedArgs ac = a;
+    ac.img = static_cast<const uint8_t*>(a.img) + f0 * fbytes;
+    ac.nframes = (uint32_t)(f1 - f0);
+    ac.zr_counts = a.zr_counts + g0;
+    ac.zr_off = off + g0;
+    ac.zr_c8 = a.zr_c8 + g0 * 64 * S8;
+    ac.zr_c16 = a.zr_c16 + g0 * 64 * S8;
+    ac.zr_cflag = a.zr_cflag + g0;
+    count(ac);
+    if ((e = launch_exclusive_scan_i32_carry(ac.zr_counts, len, agg, off + g0, s)) != hipSuccess)
+      return e;
+    if ((e = hipEventRecord(P.ev[j], s)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(P.aux, P.ev[j], 0)) != hipSuccess) return e;
+    k<<<resident_grid(k, (len + 3) / 4), 256, 0, P.aux>>>(ac, len, ac.zr_counts, ac.zr_off, ac.zr_cflag);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  join.armed = false;
+  if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux)) != hipSuccess) return e;
+  return hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0);
+}
+
 template <typename TI, int C, bool DUP, bool CM>
 static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* nsym,
                                   hipStream_t s) {
@@ -2117,11 +2180,28 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
     a.zr_c16 = c16buf;
     a.zr_cflag = cflag;
     a.zr_cbad = cbad;
+  }
+  const int64_t gpf = (int64_t)a0.h * tpr * NG;                // groups per frame
+  const int K = (e == hipSuccess && c8) ? sym_chunks(a.nframes, ngroups, gpf) : 1;
+  if (K > 1) {
+    FusedArgs ap = a;
+    ap.tpr = (int)tpr;                    // the emitter's group_loc tiles of NG groups
+    e = intra_symbols_pipelined<C, DUP, NG>(
+        ap, gpf, K, agg, [&](const FusedArgs& ac) { launch_fused_zr<TI, C, DUP, CM, OUT_COUNT>(ac, t, s); }, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(nsym, off + ngroups, 8, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) {
+      // the fused emission pass over every frame, only when the emitters stood down (*cbad)
+      a.zr_gate = cbad;
+      if (a.zr_hist) launch_fused_zr<TI, C, DUP, CM, OUT_SYMH>(a, t, s);
+      else launch_fused_zr<TI, C, DUP, CM, OUT_SYMBOLS>(a, t, s);
+      e = hipGetLastError();
+    }
+  } else if (e == hipSuccess) {
     launch_fused_zr<TI, C, DUP, CM, OUT_COUNT>(a, t, s);
     e = launch_exclusive_scan_i32(counts, ngroups, agg, off, s);
   }
-  if (e == hipSuccess) e = hipMemcpyAsync(nsym, off + ngroups, 8, hipMemcpyDeviceToDevice, s);
-  if (e == hipSuccess && a.zr_cap > 0) {
+  if (K <= 1 && e == hipSuccess) e = hipMemcpyAsync(nsym, off + ngroups, 8, hipMemcpyDeviceToDevice, s);
+  if (K <= 1 && e == hipSuccess && a.zr_cap > 0) {
     if (c8) {
       // the emitter; the fused emission pass only when the emitter stood down (*cbad)
       auto k = a.zr_hist ? sym_emit_kernel<C, DUP, true, NG> : sym_emit_kernel<C, DUP, false, NG>;

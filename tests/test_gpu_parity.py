@@ -1210,6 +1210,47 @@ def test_intra_symbols_emission_histogram(case):
         assert (np.abs(want[want != 4000]) >= 512).any()
 
 
+@pytest.mark.parametrize("case,chunks", [("s1", 2), ("s1", 5), ("s007", 3), ("s0005", 2),
+                                        ("rgb", 4), ("ragged", 5), ("odd_rows", 3)])
+def test_intra_symbols_pipelined_chunks(monkeypatch, case, chunks):
+    """The count pass and the emitter pipelined over chunks of whole frames
+    (IVC_SYM_FORCE_CHUNKS; the bench's 256 x 4K call takes 16): stream, length and emission
+    histogram equal the oracle's for every hand-off tier (s007: int16 slots; s0005: the
+    emitters stand down and the fused emission pass runs over every frame), a capacity-cut
+    stream, and a frame whose group count is not a multiple of 4 (odd_rows: one chunk)."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    monkeypatch.setenv("IVC_SYM_FORCE_CHUNKS", str(chunks))
+    rng = np.random.default_rng(chunks * 31 + len(case))
+    F, H, W, C = 5, 48, 128, 1
+    scale = {"s007": 0.07, "s0005": 0.0005}.get(case, 1.0)
+    if case == "rgb":
+        C = 3
+    if case == "ragged":
+        W = 264                                     # 33 blocks: the last group holds 1 block
+    if case == "odd_rows":
+        H = 40                                      # 5 block rows: 10 groups per frame
+    img = rng.integers(0, 256, (F, H, W, C), dtype=np.uint8)
+    img[:, :16] = img[:, :1, :1]
+    img[2] = 128                                    # a flat frame inside a chunk
+    table = PatchQuant(scale).get_quantization_table().astype(np.float64)
+    want = _zr_chain(img, table)
+    fr = torch.from_numpy(img if C == 3 else img[..., 0]).cuda()
+    nsym = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out = torch.full((want.size,), -1, dtype=torch.int32, device="cuda")
+    hist = torch.zeros(8194, dtype=torch.int64, device="cuda")
+    D.intra_symbols(fr, table, out, nsym, hist=hist, hist_lo=-4097)
+    torch.cuda.synchronize()
+    assert int(nsym.item()) == want.size
+    assert_bits(out.cpu().numpy(), want, (case, chunks))
+    assert np.array_equal(hist.cpu().numpy(), O.histogram(want, -4097, 8194)), (case, chunks)
+    cut = torch.full((want.size // 3,), -1, dtype=torch.int32, device="cuda")
+    D.intra_symbols(fr, table, cut, nsym)
+    torch.cuda.synchronize()
+    assert int(nsym.item()) == want.size
+    assert np.array_equal(cut.cpu().numpy(), want[:want.size // 3])
+
+
 @pytest.mark.parametrize("shift", [1, 2, 3])
 def test_intra_symbols_unaligned_stream(shift):
     """The fused emit's 16-byte stores when the output view starts 4/8/12 bytes past a 16-byte
