@@ -2083,8 +2083,8 @@ static void launch_fused_zr(const FusedArgs& a_in, const QTab& t, hipStream_t s)
 }
 
 // The count pass and the emitter pipelined over K chunks of whole frames (like the zero-run
-// encode, ivc_entropy.hip): chunk j's count pass and its scan (continuing chunk j - 1's total)
-// on the caller's stream, chunk j's emission on the second stream once its offsets exist.  A
+// encode, ivc_entropy.hip): chunk j's count pass on the caller's stream, its scan (continuing
+// chunk j - 1's total) and then its emission on the second stream.  A
 // chunk's groups are contiguous (frame-major group numbering), so every per-group array is
 // addressed from the chunk's first group; chunks start on whole block rows, so the emitter's
 // column bookkeeping is unchanged.
@@ -2133,10 +2133,12 @@ static hipError_t intra_symbols_pipelined(const FusedArgs& a, int64_t gpf, int K
     ac.zr_c16 = a.zr_c16 + g0 * 64 * S8;
     ac.zr_cflag = a.zr_cflag + g0;
     count(ac);
-    if ((e = launch_exclusive_scan_i32_carry(ac.zr_counts, len, agg, off + g0, s)) != hipSuccess)
-      return e;
+    // the scan on the second stream, ahead of its emitter: the caller's stream runs the count
+    // passes back to back
     if ((e = hipEventRecord(P.ev[j], s)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(P.aux, P.ev[j], 0)) != hipSuccess) return e;
+    if ((e = launch_exclusive_scan_i32_carry(ac.zr_counts, len, agg, off + g0, P.aux)) != hipSuccess)
+      return e;
     k<<<resident_grid(k, (len + 3) / 4), 256, 0, P.aux>>>(ac, len, ac.zr_counts, ac.zr_off, ac.zr_cflag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
