@@ -891,13 +891,19 @@ hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int
 #ifndef IVC_ZR_CHUNKS
 #define IVC_ZR_CHUNKS 32
 #endif
+#ifndef IVC_ZR_MIN_CHUNK
+#define IVC_ZR_MIN_CHUNK 98304
+#endif
 hipError_t launch_zerorun_encode(const int32_t* src, int64_t nblk, int stride, int B, int32_t eob,
                                  void* scratch, int64_t* off, int32_t* out, int64_t capacity,
                                  hipStream_t s) {
   const int64_t ng = (nblk + ZW_BLK - 1) / ZW_BLK;
   int K = IVC_ZR_CHUNKS;
   if (K > PIPE_EVENTS - 2) K = PIPE_EVENTS - 2;
-  if (ng < 2048 * (int64_t)K) K = 1;
+  // groups per chunk at least (64 x 4K frames: 3.02 ms unpipelined, 2.85 with 16 chunks of 97 K
+  // groups, 3.15 with 32 of 48 K — profiles/r04aq_ab_small_batch.log)
+  if (ng / IVC_ZR_MIN_CHUNK < K) K = (int)(ng / IVC_ZR_MIN_CHUNK);
+  if (K < 1) K = 1;
   const char* f = getenv("IVC_ZR_FORCE_CHUNKS");   // test hook (per call): K chunks, any size
   if (f && f[0]) K = std::max(1, std::min(atoi(f), PIPE_EVENTS - 2));
   if (!IVC_ZC || !zw_ok(src, stride, B)) K = 1;
@@ -1464,6 +1470,9 @@ __global__ void s2i_rejected_verdict(const int* ok, int64_t* err) {
 #ifndef IVC_S2I_CHUNKS
 #define IVC_S2I_CHUNKS 32
 #endif
+#ifndef IVC_S2I_MIN_CHUNK
+#define IVC_S2I_MIN_CHUNK 16384
+#endif
 static int s2i_chunks(int64_t ntf) {
   // test hook (read per call): IVC_S2I_FORCE_CHUNKS=K pipelines any stream of >= K tiles
   const char* f = getenv("IVC_S2I_FORCE_CHUNKS");
@@ -1475,7 +1484,9 @@ static int s2i_chunks(int64_t ntf) {
   }
   int K = IVC_S2I_CHUNKS;
   if (K > S2I_MAX_CHUNKS) K = S2I_MAX_CHUNKS;
-  if (ntf < 64 * (int64_t)K) K = 1;          // small streams: one pass
+  // stream tiles per chunk at least (64 x 4K frames, 216 K tiles: 4.25 ms in one pass, 4.10
+  // with 8 or 16 chunks, 4.18 with 32 — profiles/r04ar_ab64_decode_chunks.log)
+  if (ntf / IVC_S2I_MIN_CHUNK < K) K = (int)(ntf / IVC_S2I_MIN_CHUNK);
   return K < 1 ? 1 : K;
 }
 

@@ -2091,10 +2091,17 @@ static void launch_fused_zr(const FusedArgs& a_in, const QTab& t, hipStream_t s)
 #ifndef IVC_SYM_CHUNKS
 #define IVC_SYM_CHUNKS 16
 #endif
+// groups per chunk at least: smaller chunks measured slower than no pipelining (64 x 4K frames:
+// 2.18 ms unpipelined, 2.08 with 4 chunks of 259 K groups, 2.45 with 8, 3.34 with 16 —
+// profiles/r04aq_ab_small_batch.log; 256 frames: 20 chunks of 207 K groups fine, 24 of 173 K not)
+#ifndef IVC_SYM_MIN_CHUNK
+#define IVC_SYM_MIN_CHUNK 196608
+#endif
 static int sym_chunks(int64_t nframes, int64_t ngroups, int64_t gpf) {
   int K = IVC_SYM_CHUNKS;
   if (K > PIPE_EVENTS - 2) K = PIPE_EVENTS - 2;
-  if (ngroups < 2048 * (int64_t)K) K = 1;
+  if (ngroups / IVC_SYM_MIN_CHUNK < K) K = (int)(ngroups / IVC_SYM_MIN_CHUNK);
+  if (K < 1) K = 1;
   const char* f = getenv("IVC_SYM_FORCE_CHUNKS");   // test hook (per call): K chunks, any size
   if (f && f[0]) K = std::max(1, std::min(atoi(f), PIPE_EVENTS - 2));
   if (K > nframes) K = (int)nframes;
