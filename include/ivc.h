@@ -52,9 +52,25 @@ enum ivc_status {
 /* ---------------------------------------------------------------- runtime ---------- */
 const char* ivc_last_error(void);
 int ivc_version(void);
-/* 1 if the exact-u8 +-16 motion search runs on the matrix cores (me_mfma16_kernel; environment
-   IVC_ME_MFMA=0 selects the dot4 search me_tile16_kernel), 0 otherwise */
+/* 1: the exact-u8 +-16 motion search runs on the matrix cores (me_mfma16x2_kernel); it is the
+   only +-16 exact-u8 search the library ships (kept for callers that probed it) */
 int ivc_me_mfma_enabled(void);
+/* Pipeline tuning overrides (process-wide, thread-safe; replace environment test hooks, so a
+ * stray variable in the caller's environment never changes a call).  value 0 restores the
+ * library's own choice.  Chunk counts force the number of pipelined chunks (any chunk size,
+ * clamped to what the call allows); IVC_TUNE_S2I_NO_FALLBACK = 1 makes symbols -> image report
+ * err[0] = -100 instead of running the general decoder when the fused parse rejects.      */
+enum ivc_tuning_key {
+  IVC_TUNE_ZR_CHUNKS = 0,        /* ZeroRunCoder.encode (ivc_zerorun_encode*)              */
+  IVC_TUNE_SYM_CHUNKS = 1,       /* pixels -> symbols (ivc_intra_symbols*)                 */
+  IVC_TUNE_S2I_CHUNKS = 2,       /* symbols -> image (ivc_symbols2image*)                  */
+  IVC_TUNE_INTER_CHUNKS = 3,     /* fused inter encode (ivc_inter_encode*)                 */
+  IVC_TUNE_S2I_NO_FALLBACK = 4,
+  IVC_TUNE_COUNT = 5
+};
+int ivc_set_tuning(int key, int value);
+/* the current override of `key` (0: none), or IVC_E_ARG for an unknown key */
+int ivc_tuning(int key);
 int ivc_device_count(void);
 int ivc_set_device(int device);
 /* 1 if the loaded code object matches the current device (gfx950), 0 otherwise */
@@ -65,6 +81,8 @@ int ivc_device_ok(void);
  * 0 (the default: a half-duplex host link gains nothing from it) runs every call in one
  * piece.  Process-wide.                                                                   */
 int ivc_set_host_pipeline(int64_t chunk_bytes);
+/* the current chunk size of ivc_set_host_pipeline (0: off) */
+int64_t ivc_host_pipeline(void);
 /* release the library's cached scratch buffers on the current device, and the pinned host
  * blocks ivc_host_free has cached (process-wide)                                          */
 int ivc_release_scratch(void);

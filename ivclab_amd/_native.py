@@ -57,6 +57,9 @@ _SIGS = {
     "ivc_dct8x8_dev": ([_P, _I, _L, _P, _I, _I, _I, _P], _I),
     "ivc_dct8x8_image": ([_P, _I, _L, _L, _L, _P, _I, _I, _I], _I),
     "ivc_set_host_pipeline": ([_L], _I),
+    "ivc_host_pipeline": ([], _L),
+    "ivc_set_tuning": ([_I, _I], _I),
+    "ivc_tuning": ([_I], _I),
     "ivc_dct8x8_image_dev": ([_P, _I, _L, _L, _L, _P, _I, _I, _I, _P], _I),
     "ivc_quantize": ([_P, _I, _L, _I, _P, _I, _P], _I),
     "ivc_quantize_dev": ([_P, _I, _L, _I, _P, _I, _P, _P], _I),
@@ -240,6 +243,20 @@ def empty(shape, dtype) -> np.ndarray:
 def empty_like(a) -> np.ndarray:
     a = np.asarray(a)
     return empty(a.shape, a.dtype)
+
+
+# ivc_set_tuning keys (include/ivc.h enum ivc_tuning_key)
+TUNE = {"zr_chunks": 0, "sym_chunks": 1, "s2i_chunks": 2, "inter_chunks": 3, "s2i_no_fallback": 4}
+
+
+def set_tuning(name: str, value: int) -> int:
+    """Set one pipeline tuning override (0 restores the library's choice); returns the previous
+    value."""
+    L = lib()
+    key = TUNE[name]
+    prev = int(L.ivc_tuning(key))
+    check(L.ivc_set_tuning(key, int(value)), "ivc_set_tuning")
+    return prev
 
 
 def table_arg(table: np.ndarray) -> np.ndarray:

@@ -18,6 +18,12 @@
 
 #include "ivc_internal.h"
 
+namespace ivc {
+// ivc_set_tuning overrides, read once per call by the launchers
+std::atomic<int> g_tuning[IVC_TUNE_COUNT] = {};
+int tuning(int key) { return g_tuning[key].load(std::memory_order_relaxed); }
+}  // namespace ivc
+
 using namespace ivc;
 
 namespace {
@@ -453,7 +459,7 @@ extern "C" {
 
 const char* ivc_last_error(void) { return g_err.c_str(); }
 int ivc_version(void) { return 10000; }
-int ivc_me_mfma_enabled(void) { return me_use_mfma() ? 1 : 0; }
+int ivc_me_mfma_enabled(void) { return 1; }
 
 int ivc_device_count(void) {
   int n = 0;
@@ -521,6 +527,20 @@ int ivc_set_host_pipeline(int64_t chunk_bytes) {
   if (chunk_bytes < 0) return fail(IVC_E_ARG, "ivc_set_host_pipeline: chunk must be >= 0");
   g_pipe_chunk.store((size_t)chunk_bytes, std::memory_order_relaxed);
   return IVC_OK;
+}
+
+int64_t ivc_host_pipeline(void) { return (int64_t)g_pipe_chunk.load(std::memory_order_relaxed); }
+
+int ivc_set_tuning(int key, int value) {
+  if (key < 0 || key >= IVC_TUNE_COUNT) return fail(IVC_E_ARG, "ivc_set_tuning: unknown key");
+  if (value < 0) return fail(IVC_E_ARG, "ivc_set_tuning: value must be >= 0");
+  ivc::g_tuning[key].store(value, std::memory_order_relaxed);
+  return IVC_OK;
+}
+
+int ivc_tuning(int key) {
+  if (key < 0 || key >= IVC_TUNE_COUNT) return fail(IVC_E_ARG, "ivc_tuning: unknown key");
+  return ivc::g_tuning[key].load(std::memory_order_relaxed);
 }
 
 int ivc_set_store_pace(double total_gbps) {
@@ -1030,7 +1050,7 @@ static int inter_encode_enqueue(const uint8_t* frames, int64_t nframes, int64_t 
                                 int32_t hist_lo, int32_t hist_n, hipStream_t s) {
   const int64_t HW = H * W, npairs = nframes - 1, hw = (H / 8) * (W / 8);
   int K = IVC_INTER_CHUNKS;
-  if (const char* f = getenv("IVC_INTER_FORCE_CHUNKS")) K = atoi(f);   // test hook, per call
+  if (const int f = tuning(IVC_TUNE_INTER_CHUNKS)) K = f;               // ivc_set_tuning
   if (K > PIPE_EVENTS - 2) K = PIPE_EVENTS - 2;
   if (K > npairs) K = (int)npairs;
   auto residual = [&](int64_t p0, int64_t p1, hipStream_t st) {

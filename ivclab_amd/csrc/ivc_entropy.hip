@@ -904,8 +904,7 @@ hipError_t launch_zerorun_encode(const int32_t* src, int64_t nblk, int stride, i
   // groups, 3.15 with 32 of 48 K — profiles/r04aq_ab_small_batch.log)
   if (ng / IVC_ZR_MIN_CHUNK < K) K = (int)(ng / IVC_ZR_MIN_CHUNK);
   if (K < 1) K = 1;
-  const char* f = getenv("IVC_ZR_FORCE_CHUNKS");   // test hook (per call): K chunks, any size
-  if (f && f[0]) K = std::max(1, std::min(atoi(f), PIPE_EVENTS - 2));
+  if (const int f = tuning(IVC_TUNE_ZR_CHUNKS)) K = std::min(f, PIPE_EVENTS - 2);  // any size
   if (!IVC_ZC || !zw_ok(src, stride, B)) K = 1;
   if (K <= 1) {
     hipError_t e = launch_zerorun_offsets(src, nblk, stride, B, scratch, off, s);
@@ -1446,13 +1445,8 @@ int64_t sym_image_scratch_bytes(int64_t n, int64_t ngroups) {
   return bytes;
 }
 
-// test hook (see launch_symbols2image)
-static bool s2i_no_fallback() {
-  // read per call (a getenv, negligible next to the call): a test can set and clear it
-  // between calls in one process
-  const char* nf = getenv("IVC_S2I_NO_FALLBACK");
-  return nf && nf[0] == '1';
-}
+// ivc_set_tuning(IVC_TUNE_S2I_NO_FALLBACK, 1) (see launch_symbols2image)
+static bool s2i_no_fallback() { return tuning(IVC_TUNE_S2I_NO_FALLBACK) == 1; }
 
 constexpr int64_t IVC_S2I_REJECTED = -100;
 __global__ void s2i_rejected_verdict(const int* ok, int64_t* err) {
@@ -1474,10 +1468,9 @@ __global__ void s2i_rejected_verdict(const int* ok, int64_t* err) {
 #define IVC_S2I_MIN_CHUNK 16384
 #endif
 static int s2i_chunks(int64_t ntf) {
-  // test hook (read per call): IVC_S2I_FORCE_CHUNKS=K pipelines any stream of >= K tiles
-  const char* f = getenv("IVC_S2I_FORCE_CHUNKS");
-  if (f && f[0]) {
-    int K = atoi(f);
+  // ivc_set_tuning(IVC_TUNE_S2I_CHUNKS, K) pipelines any stream of >= K tiles
+  if (const int f = tuning(IVC_TUNE_S2I_CHUNKS)) {
+    int K = f;
     if (K > S2I_MAX_CHUNKS) K = S2I_MAX_CHUNKS;
     if (ntf < K) K = (int)ntf;
     return K < 1 ? 1 : K;
@@ -1569,7 +1562,7 @@ hipError_t launch_symbols2image(const int32_t* sym, int64_t n, int64_t nframes, 
     zf_finish<<<1, 1, 0, s>>>(z.flags, z.tile_first + ntf, expected, z.flags + 1, err);
     skip = z.flags + 1;
   }
-  // (IVC_S2I_NO_FALLBACK=1, a test hook: the fused kernel's image stands alone, so a test can
+  // (ivc_set_tuning(IVC_TUNE_S2I_NO_FALLBACK, 1): the fused kernel's image stands alone, so a test can
   // tell that it — not the general path — produced the image; when the fused path rejects the
   // stream, err[0] = IVC_S2I_REJECTED instead of the general decoder's verdict)
   if (skip && s2i_no_fallback()) {

@@ -38,6 +38,9 @@ struct QTab {
   double q[192];
 };
 
+// ivc_set_tuning overrides (ivc_capi.hip): 0 = the library's own choice
+int tuning(int key);
+
 // error raised by a launcher; turned into a status + message by the C-ABI layer
 struct Error {
   int code;
@@ -149,9 +152,8 @@ hipError_t launch_histogram(const int32_t* sym, int64_t n, int32_t lo, int32_t n
 hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, int64_t nframes,
                                   int64_t H, int64_t W, int sr, int mode, int64_t* mv,
                                   hipStream_t s);
-// the exact-u8 +-16 search runs on the matrix cores (IVC_ME_MFMA, default on)
-bool me_use_mfma();
-// the matrix-core +-16 search of a batch (ivc_me_mfma.hip); false: not applicable
+// the matrix-core +-16 search of a batch (ivc_me_mfma.hip); false: not applicable (a frame of
+// 2 GiB or more)
 bool launch_me_mfma16(const uint8_t* ref, const uint8_t* cur, int64_t nf, int H, int W, int64_t* mv,
                       hipStream_t s);
 hipError_t launch_motion_compensate(const void* ref, int esize, int64_t nframes, int64_t H,

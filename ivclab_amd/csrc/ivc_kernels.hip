@@ -2102,11 +2102,22 @@ static int sym_chunks(int64_t nframes, int64_t ngroups, int64_t gpf) {
   if (K > PIPE_EVENTS - 2) K = PIPE_EVENTS - 2;
   if (ngroups / IVC_SYM_MIN_CHUNK < K) K = (int)(ngroups / IVC_SYM_MIN_CHUNK);
   if (K < 1) K = 1;
-  const char* f = getenv("IVC_SYM_FORCE_CHUNKS");   // test hook (per call): K chunks, any size
-  if (f && f[0]) K = std::max(1, std::min(atoi(f), PIPE_EVENTS - 2));
+  if (const int f = tuning(IVC_TUNE_SYM_CHUNKS)) K = std::min(f, PIPE_EVENTS - 2);  // any size
   if (K > nframes) K = (int)nframes;
   if (gpf % 4 != 0) K = 1;                           // the emitter reads the flags 4 at a time
   return K;
+}
+
+// hist[i] += part[i] when the count passes found no value outside int16 (*gate == 0): the
+// pipelined emitters' histogram joins the caller's only once every chunk's count pass has
+// run, so an emitter that started before a later chunk set cbad never reaches hist (the fused
+// OUT_SYMH pass, gated the other way, then counts every frame)
+__global__ __launch_bounds__(256) void hist_gated_add_kernel(unsigned long long* __restrict__ hist,
+                                                             const unsigned long long* __restrict__ part,
+                                                             int32_t n, const int* __restrict__ gate) {
+  if (*gate) return;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256)
+    if (part[i]) hist[i] += part[i];
 }
 
 template <int C, bool DUP, int NG, typename CountFn>
@@ -2121,6 +2132,20 @@ static hipError_t intra_symbols_pipelined(const FusedArgs& a, int64_t gpf, int K
   std::lock_guard<std::mutex> lock(P.mu);
   int64_t* off = const_cast<int64_t*>(a.zr_off);
   if ((e = hipMemsetAsync(off, 0, 8, s)) != hipSuccess) return e;
+  // the emitters' histogram goes to a scratch copy, added to hist after the join (above)
+  unsigned long long* hpart = nullptr;
+  if (a.zr_hist) {
+    if ((e = scratch_alloc((void**)&hpart, (size_t)a.zr_hist_n * 8, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(hpart, 0, (size_t)a.zr_hist_n * 8, s)) != hipSuccess) {
+      (void)hipFreeAsync(hpart, s);
+      return e;
+    }
+  }
+  struct FreeOnExit {
+    void* p;
+    hipStream_t s;
+    ~FreeOnExit() { if (p) (void)hipFreeAsync(p, s); }
+  } hfree{hpart, s};
   if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 2], s)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(P.aux, P.ev[PIPE_EVENTS - 2], 0)) != hipSuccess) return e;
   PipeJoin join{P, s, true};
@@ -2132,6 +2157,7 @@ static hipError_t intra_symbols_pipelined(const FusedArgs& a, int64_t gpf, int K
     if (f1 <= f0) break;
     const int64_t g0 = f0 * gpf, len = (f1 - f0) * gpf;
     FusedArgs ac = a;
+    if (hpart) ac.zr_hist = hpart;
     ac.img = static_cast<const uint8_t*>(a.img) + f0 * fbytes;
     ac.nframes = (uint32_t)(f1 - f0);
     ac.zr_counts = a.zr_counts + g0;
@@ -2151,7 +2177,13 @@ static hipError_t intra_symbols_pipelined(const FusedArgs& a, int64_t gpf, int K
   }
   join.armed = false;
   if ((e = hipEventRecord(P.ev[PIPE_EVENTS - 1], P.aux)) != hipSuccess) return e;
-  return hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0);
+  if ((e = hipStreamWaitEvent(s, P.ev[PIPE_EVENTS - 1], 0)) != hipSuccess) return e;
+  if (hpart) {
+    hist_gated_add_kernel<<<(a.zr_hist_n + 255) / 256 < 1024 ? (a.zr_hist_n + 255) / 256 : 1024, 256, 0, s>>>(
+        a.zr_hist, hpart, a.zr_hist_n, a.zr_cbad);
+    e = hipGetLastError();
+  }
+  return e;
 }
 
 template <typename TI, int C, bool DUP, bool CM>
@@ -2166,7 +2198,7 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
   int64_t* off = nullptr;
   constexpr int NP = (C == 1 && DUP) ? 2 : 3;
   // the coefficient hand-off (IVC_EMIT_C8): only when the stream is emitted
-  const bool c8 = IVC_EMIT_C8 && a.zr_cap > 0;
+  bool c8 = IVC_EMIT_C8 && a.zr_cap > 0;
   int8_t* c8buf = nullptr;
   int16_t* c16buf = nullptr;
   uint8_t* cflag = nullptr;
@@ -2174,13 +2206,22 @@ static hipError_t intra_symbols_t(const FusedArgs& a0, const QTab& t, int64_t* n
   hipError_t e = scratch_alloc((void**)&counts, (size_t)ngroups * 4, s);
   if (e == hipSuccess) e = scratch_alloc((void**)&agg, (size_t)scan_scratch_elems(ngroups) * 8, s);
   if (e == hipSuccess) e = scratch_alloc((void**)&off, (size_t)(ngroups + 1) * 8, s);
-  if (c8) {
+  if (c8 && e == hipSuccess) {
     const size_t per = (size_t)64 * c8_stride(NP);
-    if (e == hipSuccess) e = scratch_alloc((void**)&c8buf, (size_t)ngroups * per, s);
-    if (e == hipSuccess) e = scratch_alloc((void**)&c16buf, (size_t)ngroups * 2 * per, s);
-    if (e == hipSuccess) e = scratch_alloc((void**)&cflag, (size_t)ngroups + 16, s);
-    if (e == hipSuccess) e = scratch_alloc((void**)&cbad, 16, s);
-    if (e == hipSuccess) e = hipMemsetAsync(cbad, 0, 16, s);
+    hipError_t e8 = scratch_alloc((void**)&c8buf, (size_t)ngroups * per, s);
+    if (e8 == hipSuccess) e8 = scratch_alloc((void**)&c16buf, (size_t)ngroups * 2 * per, s);
+    if (e8 == hipSuccess) e8 = scratch_alloc((void**)&cflag, (size_t)ngroups + 16, s);
+    if (e8 == hipSuccess) e8 = scratch_alloc((void**)&cbad, 16, s);
+    if (e8 == hipSuccess) e8 = hipMemsetAsync(cbad, 0, 16, s);
+    if (e8 != hipSuccess) {
+      // no room for the hand-off: the path without it (count pass, scan, fused emission)
+      for (void** pp : {(void**)&c8buf, (void**)&c16buf, (void**)&cflag, (void**)&cbad}) {
+        if (*pp) (void)hipFreeAsync(*pp, s);
+        *pp = nullptr;
+      }
+      (void)hipGetLastError();
+      c8 = false;
+    }
   }
   if (e == hipSuccess) {
     a.zr_counts = counts;

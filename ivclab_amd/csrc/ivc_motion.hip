@@ -397,10 +397,6 @@ __device__ __forceinline__ void s2_hrow(__amdgpu_buffer_rsrc_t rs, int off, uint
   }
 }
 
-// SMAJOR: the tiled search's layout and term, -32 S2 at [f][y][x & 3][x >> 2] (each row split
-// into four planes of W/4 by x mod 4), so a lane's candidates dx = 4m + s, 4m + 4 + s, ... are
-// contiguous.
-template <bool SMAJOR>
 __global__ __launch_bounds__(256) void me_s2_kernel(const uint8_t* __restrict__ ref,
                                                     int64_t nframes, int H, int W,
                                                     int32_t* __restrict__ s2) {
@@ -418,9 +414,8 @@ __global__ __launch_bounds__(256) void me_s2_kernel(const uint8_t* __restrict__ 
     const int y1 = min(y0 + S2Y, H - 7);          // exclusive
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(ref + f * HW), 0, (int)HW, 0x00020000);
-    int32_t* out = s2 + f * HW + (SMAJOR ? xg : x);
+    int32_t* out = s2 + f * HW + x;
     const int nvalid = min(4, W - 7 - x);         // outputs of this group inside the row
-    const int W4 = W >> 2;
     uint32_t h[8][4];
     uint32_t acc[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
@@ -434,11 +429,7 @@ __global__ __launch_bounds__(256) void me_s2_kernel(const uint8_t* __restrict__ 
       for (int k = 0; k < 8; ++k) {
         const int yy = y + k;
         if (yy < y1) {
-          if (SMAJOR) {                             // -32 S2: the tiled search's key term
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-              if (s < nvalid) out[(int64_t)yy * W + s * W4] = -(int32_t)(acc[s] << 5);
-          } else if (nvalid == 4) {
+          if (nvalid == 4) {
             // 16-byte aligned: x and W are multiples of 4 and 8
             *reinterpret_cast<int4*>(out + (int64_t)yy * W) =
                 make_int4((int)acc[0], (int)acc[1], (int)acc[2], (int)acc[3]);
@@ -470,18 +461,6 @@ static unsigned me_fast_grid(const void* kernel, int64_t wgs) {
 #ifndef IVC_ME_XCD
 #define IVC_ME_XCD 1
 #endif
-#ifndef IVC_ME_TILE
-#define IVC_ME_TILE 1                      // SR = 16: tiled search (me_tile16_kernel)
-#endif
-#ifndef IVC_ME_ABL
-#define IVC_ME_ABL 0                       // diagnostic builds: bit mask of skipped phases
-#endif
-#ifndef IVC_ME_MFMA_DEFAULT
-#define IVC_ME_MFMA_DEFAULT 1
-#endif
-#ifndef IVC_ME_TILE_PREFETCH
-#define IVC_ME_TILE_PREFETCH 0
-#endif
 #ifndef IVC_ME_CHUNK_BYTES
 #define IVC_ME_CHUNK_BYTES (256LL << 20)   // S2 scratch per chunk of frame pairs
 #endif
@@ -489,20 +468,12 @@ static unsigned me_fast_grid(const void* kernel, int64_t wgs) {
 template <int SR> struct MeCfg;
 // PITCH: LDS row pitch of a staged window (dwords), chosen so a row read of a 32-lane half
 // hits distinct banks (searched offline; SR = 4 is 2-way at best with 4 blocks per wave)
-template <> struct MeCfg<16> { static constexpr int BPW = 1, NDR = 7, DYT = 5, PITCH = 21; };  // 63 of 64 lanes
 template <> struct MeCfg<8> { static constexpr int BPW = 2, NDR = 6, DYT = 3, PITCH = 9; };   // 30 of 32 lanes
 template <> struct MeCfg<4> { static constexpr int BPW = 4, NDR = 5, DYT = 2, PITCH = 5; };   // 15 of 16 lanes
 
 typedef unsigned int me_u32x4 __attribute__((ext_vector_type(4)));
 
 template <int DYT> __device__ __forceinline__ void row_fence(uint32_t (&acc)[DYT][4]);
-template <> __device__ __forceinline__ void row_fence<5>(uint32_t (&a)[5][4]) {
-  asm volatile("" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[1][0]),
-               "+v"(a[1][1]), "+v"(a[1][2]), "+v"(a[1][3]), "+v"(a[2][0]), "+v"(a[2][1]),
-               "+v"(a[2][2]), "+v"(a[2][3]), "+v"(a[3][0]), "+v"(a[3][1]), "+v"(a[3][2]),
-               "+v"(a[3][3]), "+v"(a[4][0]), "+v"(a[4][1]), "+v"(a[4][2]), "+v"(a[4][3])
-               :: "memory");
-}
 template <> __device__ __forceinline__ void row_fence<3>(uint32_t (&a)[3][4]) {
   asm volatile("" : "+v"(a[0][0]), "+v"(a[0][1]), "+v"(a[0][2]), "+v"(a[0][3]), "+v"(a[1][0]),
                "+v"(a[1][1]), "+v"(a[1][2]), "+v"(a[1][3]), "+v"(a[2][0]), "+v"(a[2][1]),
@@ -717,270 +688,6 @@ __global__ __launch_bounds__(256) void me_fast_u8_kernel(const uint8_t* __restri
   }
 }
 
-// ---------------------------------------------------------------- tiled exact u8 search, SR = 16
-// A workgroup (4 waves) owns a tile of TB = 16 horizontally adjacent blocks of one block row.
-// The tile's reference rows (40 rows x 41 dwords around its blocks) are staged once in LDS as
-// four byte-shifted copies, copy_s[row][x] = bytes 4x + s .. 4x + s + 3 of the row, so
-// candidate dx = 4m + s of block j reads the aligned words copy_s[row][2j + m] and [.. + 1]:
-// the byte shifts cost 6 v_alignbyte per staged dword pair and tile instead of 6 per lane,
-// reference row and block (me_fast_u8_kernel), and all 16 blocks share one staged window.
-// Lane (g, dr) of a wave evaluates candidates dx = 4(m0 + k) + s (k = 0..3; (s, m0) from g)
-// x dy = 5 dr .. 5 dr + 4 for each of the wave's 4 blocks of the tile; S2 comes s-major
-// (me_s2_kernel<true>), so a lane's 4 S2 values per dy are contiguous.  Two barriers per
-// tile: the tile's copies are written from registers the previous iteration prefetched, and
-// the next tile's rows are loaded while this one is searched.
-namespace ts {
-constexpr int SR = 16, N = 2 * SR + 1, TB = 16, WPT = TB / 4;  // blocks per tile / per wave
-constexpr int DYT = 5;                   // dy per lane; 7 dy ranges x 9 dx groups = 63 lanes
-constexpr int ROWS = 2 * SR + 8;         // reference rows of a tile (40)
-constexpr int CW = 2 * TB + 8;           // copy words per row in use (block j: 2j .. 2j + 9)
-constexpr int PITCH = 42;                // copy row pitch (dwords)
-constexpr int NPAIR = CW / 2;            // staged word pairs per row
-constexpr int ITEMS = ROWS * NPAIR;      // staging items per tile (row, pair)
-constexpr int IPT = (ITEMS + 255) / 256; // per thread
-// Copy bases (dwords).  A row read is 3 ds_read_b64 per lane; with pitch 42 and lanes
-// (g = lane % 9, dr = lane / 9), the nine groups' (base/2 + 2 m0/4) mod 32 are 0..8 and the dy
-// ranges step 5 * 21 = 9 (mod 32) apart, so each half-wave's 32 reads hit 64 distinct banks.
-constexpr int B0 = 0, B1 = 1730, B2 = 3466, B3 = 5196;
-constexpr int CB = B3 + (ROWS + 2) * PITCH;  // current blocks (16 dwords each), after the 2
-                                              // rows past copy 3 that the dr = 6 lanes read
-constexpr int LDS_DW = CB + TB * 16;
-static_assert(B1 >= B0 + ROWS * PITCH && B2 >= B1 + ROWS * PITCH && B3 >= B2 + ROWS * PITCH, "copies");
-static_assert(CW <= PITCH, "pitch");
-}  // namespace ts
-
-typedef unsigned int me_u32x2 __attribute__((ext_vector_type(2)));
-
-// minimum over the 64 lanes (all active): DPP within rows of 16, then the 4 rows' lane 0 / 15
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));   // quad_perm 2,3,0,1
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));  // row_half_mirror
-  v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xf, 0xf, false));  // row_mirror
-  const uint32_t a = __builtin_amdgcn_readlane(v, 0), b = __builtin_amdgcn_readlane(v, 16);
-  const uint32_t c = __builtin_amdgcn_readlane(v, 32), d = __builtin_amdgcn_readlane(v, 48);
-  return min(min(a, b), min(c, d));
-}
-
-#ifndef IVC_ME_TILE_WAVES
-#define IVC_ME_TILE_WAVES 1                // min waves per SIMD the register allocation keeps
-#endif
-__global__ __launch_bounds__(256, IVC_ME_TILE_WAVES) void me_tile16_kernel(const uint8_t* __restrict__ ref,
-                                                        const uint8_t* __restrict__ cur,
-                                                        const int32_t* __restrict__ s2,
-                                                        int64_t nframes, int H, int W,
-                                                        int64_t* __restrict__ mv) {
-  using namespace ts;
-  __shared__ __attribute__((aligned(16))) uint32_t lds[LDS_DW];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = (int)__builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
-  const int h = H / 8, w = W / 8;
-  const int tpr = (w + TB - 1) / TB;                     // tiles per block row
-  const uint32_t tpf = (uint32_t)(h * tpr);
-  const uint32_t ntiles = (uint32_t)nframes * tpf;
-  const int64_t HW = (int64_t)H * W;
-  const int W4 = W >> 2;
-  // lane role; lane 63 repeats lane 54's rows (in range) and is excluded at selection
-  const int g = lane % 9, dr = min(lane / 9, 6);
-  const int s = g < 3 ? 0 : (g - 1) >> 1;
-  const int m0 = g < 3 ? 4 * g : 4 * ((g - 1) & 1);
-  const int dy0 = DYT * dr;
-  const uint32_t* const cbase =
-      lds + (s == 0 ? B0 : s == 1 ? B1 : s == 2 ? B2 : B3) + dy0 * PITCH + m0;
-
-  // the tile's reference rows as (row, word pair) items: raw dwords 2p .. 2p + 2 of the row
-  // starting at x = 8 bx0 - SR (rows outside the frame read zeros; columns outside it wrap into
-  // a neighbouring row and only feed candidates masked at selection), and its current blocks
-  auto load_tile = [&](uint32_t t, bool exists, uint32_t (&raw)[IPT][3], uint32_t& craw) {
-    const uint32_t tt = exists ? t : 0u;
-    const uint32_t f = tt / tpf;
-    const uint32_t rem = tt - f * tpf;
-    const int by = (int)(rem / (uint32_t)tpr);
-    const int bx0 = (int)(rem - (uint32_t)by * tpr) * TB;
-    const __amdgpu_buffer_rsrc_t rr = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(ref + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint8_t*>(cur + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
-#pragma unroll
-    for (int r = 0; r < IPT; ++r) {
-      const int i = tid + 256 * r;
-      const int row = i / NPAIR, p = i - row * NPAIR;
-      const int y = 8 * by - SR + row;
-      const bool ok = i < ITEMS && y >= 0 && y < H;
-      const int off = ok ? y * W + 8 * bx0 - SR + 8 * p : 0x40000000;
-      const me_u32x2 a = __builtin_amdgcn_raw_buffer_load_b64(rr, off, 0, 0);
-      raw[r][0] = a.x;
-      raw[r][1] = a.y;
-      raw[r][2] = __builtin_amdgcn_raw_buffer_load_b32(rr, off + 8, 0, 0);
-    }
-    const int j = tid >> 4, dw = tid & 15;
-    const int offc = bx0 + j < w ? (8 * by + (dw >> 1)) * W + 8 * (bx0 + j) + 4 * (dw & 1) : 0x40000000;
-    craw = __builtin_amdgcn_raw_buffer_load_b32(rc, offc, 0, 0);
-  };
-
-  // XCD-aware order (as in me_fast_u8_kernel): each XCD takes a contiguous run of tiles
-  uint32_t tile = blockIdx.x;
-  if (IVC_ME_XCD && (gridDim.x & 7u) == 0u) tile = (tile & 7u) * (gridDim.x >> 3) + (tile >> 3);
-  uint32_t raw[IPT][3], craw;
-  load_tile(tile, tile < ntiles, raw, craw);
-  for (; tile < ntiles; tile += gridDim.x) {
-    __syncthreads();                                       // previous tile's reads are done
-#pragma unroll
-    for (int r = 0; r < IPT; ++r) {
-      const int i = tid + 256 * r;
-      if (i < ITEMS && !(IVC_ME_ABL & 4)) {
-        const int row = i / NPAIR, p = i - row * NPAIR;
-        uint32_t* d = lds + row * PITCH + 2 * p;
-        const uint32_t w0 = raw[r][0], w1 = raw[r][1], w2 = raw[r][2];
-        *reinterpret_cast<me_u32x2*>(d + B0) = me_u32x2{w0, w1};
-        *reinterpret_cast<me_u32x2*>(d + B1) =
-            me_u32x2{__builtin_amdgcn_alignbyte(w1, w0, 1), __builtin_amdgcn_alignbyte(w2, w1, 1)};
-        *reinterpret_cast<me_u32x2*>(d + B2) =
-            me_u32x2{__builtin_amdgcn_alignbyte(w1, w0, 2), __builtin_amdgcn_alignbyte(w2, w1, 2)};
-        *reinterpret_cast<me_u32x2*>(d + B3) =
-            me_u32x2{__builtin_amdgcn_alignbyte(w1, w0, 3), __builtin_amdgcn_alignbyte(w2, w1, 3)};
-      }
-    }
-    lds[CB + tid] = craw;
-    __syncthreads();
-    if (IVC_ME_TILE_PREFETCH) {                            // the next tile's rows, in flight
-      const uint32_t nt = tile + gridDim.x;                // during this tile's search
-      load_tile(nt, nt < ntiles, raw, craw);
-    }
-
-    const uint32_t f = tile / tpf;
-    const uint32_t rem = tile - f * tpf;
-    const int by = (int)(rem / (uint32_t)tpr);
-    const int bx0 = (int)(rem - (uint32_t)by * tpr) * TB;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<int32_t*>(s2 + (int64_t)f * HW), 0, (int)(HW * 4), 0x00020000);
-    const int ry0 = 8 * by - SR + dy0;
-    bool vy[DYT];
-#pragma unroll
-    for (int d = 0; d < DYT; ++d)
-      vy[d] = dy0 + d < N && ry0 + d >= 0 && ry0 + d + 8 <= H;
-    // a lane's S2 quad of block j + 1 is 2 words past block j's: its first pair is block j's
-    // second, carried over (one 8-byte load per dy after the wave's first block)
-    me_u32x2 nsa[DYT], nsb[DYT];
-#pragma unroll 1
-    for (int jj = 0; jj < WPT; ++jj) {
-      const int j = wave * WPT + jj;
-      const int bx = bx0 + j;
-      if (bx >= w) break;                                  // wave-uniform
-      uint32_t cw[16];
-      {
-        const me_u32x4* cb = reinterpret_cast<const me_u32x4*>(lds + CB + 16 * j);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const me_u32x4 t = cb[q];
-          cw[4 * q] = t.x; cw[4 * q + 1] = t.y; cw[4 * q + 2] = t.z; cw[4 * q + 3] = t.w;
-        }
-      }
-      // column validity rides in the accumulators' start value: an invalid column (window
-      // outside the frame, or dx > 2 SR) starts at -2^24, which puts its key below -2^29
-      const int rx0 = 8 * bx - SR + 4 * m0 + s;
-      uint32_t acc[DYT][4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const bool vx = 4 * (m0 + k) + s < N && rx0 + 4 * k >= 0 && rx0 + 4 * k + 8 <= W;
-        const uint32_t c0 = vx ? 0u : 0xff000000u;
-#pragma unroll
-        for (int d = 0; d < DYT; ++d) acc[d][k] = c0;
-      }
-      // the block's -32 S2 words, issued before the search so their latency (HBM when the
-      // chunk's S2 outgrows the caches, 8K) hides behind it
-      const int qb = 2 * bx - SR / 4 + m0;                 // s-plane column of k = 0
-#pragma unroll
-      for (int d = 0; d < DYT; ++d) {
-        const int off = ((ry0 + d) * W + s * W4 + qb) * 4;
-        if (IVC_ME_ABL & 2) {
-          nsa[d] = me_u32x2{(uint32_t)off, 0u};
-          nsb[d] = me_u32x2{0u, (uint32_t)off};
-        } else {
-          nsa[d] = jj == 0 ? __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0) : nsb[d];
-          nsb[d] = __builtin_amdgcn_raw_buffer_load_b64(rs, off + 8, 0, 0);
-        }
-      }
-      const uint32_t* const wb = cbase + 2 * j;
-      // the 6 words of a row (5 used) are read one row ahead of their use, as three
-      // ds_read_b64 (volatile: merged into ds_read2_b64 they would take 4x the LDS cycles —
-      // 16-lane groups on 32 banks — and conflict on this layout)
-      auto row_words = [&](int rr, uint32_t (&v)[6]) {
-        typedef const volatile __attribute__((address_space(3))) me_u32x2 lds_u32x2;
-        lds_u32x2* p = (lds_u32x2*)(wb + rr * PITCH);
-        const me_u32x2 a = p[0], b = p[1], c = p[2];
-        v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y; v[4] = c.x; v[5] = c.y;
-      };
-      uint32_t v[6];
-      if (!(IVC_ME_ABL & 1)) row_words(0, v);
-#pragma unroll
-      for (int rr = 0; rr < ((IVC_ME_ABL & 1) ? 0 : DYT + 7); ++rr) {
-        uint32_t nv[6] = {0u, 0u, 0u, 0u, 0u, 0u};
-        if (rr + 1 < DYT + 7) row_words(rr + 1, nv);
-#pragma unroll
-        for (int d = 0; d < DYT; ++d) {
-          const int u = rr - d;                            // block row matched by this ref row
-          if (u >= 0 && u < 8) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              acc[d][k] = __builtin_amdgcn_udot4(v[k], cw[2 * u], acc[d][k], false);
-              acc[d][k] = __builtin_amdgcn_udot4(v[k + 1], cw[2 * u + 1], acc[d][k], false);
-            }
-          }
-        }
-        row_fence<DYT>(acc);                               // keep the schedule row by row
-#pragma unroll
-        for (int q = 0; q < 6; ++q) v[q] = nv[q];
-      }
-      // selection: key = 64 X - 32 S2 + 31 - rank = 32 (-K) + 31 - rank (rank = 4d + k, the
-      // raster order of the lane's candidates), so the lane's maximum key is its first strict
-      // minimum of K = S2 - 2X.  Valid keys lie in [-2^27, 2^27); an invalid column's is below
-      // -2^29 and an invalid row is skipped.  Every -32 S2 word read is a window's or zero
-      // (the scratch is cleared before the pre-pass; reads outside it return zero), so no key
-      // wraps.
-      int best = INT_MIN;
-#pragma unroll
-      for (int d = 0; d < DYT; ++d) {
-        const uint32_t ns[4] = {nsa[d].x, nsa[d].y, nsb[d].x, nsb[d].y};
-        int rm = INT_MIN;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          rm = max(rm, (int)((acc[d][k] << 6) + ns[k]) + (31 - 4 * d - k));
-        best = vy[d] ? max(best, rm) : best;
-      }
-      uint32_t bk = 0xffffffffu, bi = 0x7fffffffu;
-      if (lane < 63 && best >= -(1 << 28)) {
-        bk = (uint32_t)((1 << 30) - (best >> 5));          // K + 2^30: the minimum is the max key
-        const int r = 31 - (best & 31);
-        bi = (uint32_t)((dy0 + (r >> 2)) * N + 4 * (m0 + (r & 3)) + s);
-      }
-      // lexicographic (K, raster index) minimum over the wave: first strict minimum
-      const uint32_t mk = (IVC_ME_ABL & 8) ? bk : wave_min_u32(bk);
-      // ties on the minimum K are rare outside flat content: one lane holding it is the answer
-      const uint64_t holders = __ballot(bk == mk);
-      const uint32_t mi = (IVC_ME_ABL & 8) ? bi
-                          : __builtin_popcountll(holders) == 1
-                              ? (uint32_t)__builtin_amdgcn_readlane((int)bi, __builtin_ctzll(holders))
-                              : wave_min_u32(bk == mk ? bi : 0x7fffffffu);
-      if (lane == 0)
-        mv[((int64_t)f * h + by) * w + bx] = mi == 0x7fffffffu ? (int64_t)SR * N + SR : (int64_t)mi;
-    }
-    if (!IVC_ME_TILE_PREFETCH && !(IVC_ME_ABL & 16)) {     // fewer registers: 5 waves per SIMD
-      const uint32_t nt = tile + gridDim.x;
-      load_tile(nt, nt < ntiles, raw, craw);
-    }
-  }
-}
-
-// IVC_ME_MFMA: 1 = the matrix-core +-16 search (ivc_me_mfma.hip), 0 = the dot4 tiled search
-bool me_use_mfma() {
-  static const bool v = [] {
-    const char* e = getenv("IVC_ME_MFMA");
-    return e ? atoi(e) != 0 : IVC_ME_MFMA_DEFAULT != 0;
-  }();
-  return v;
-}
-
 hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, int64_t nframes,
                                   int64_t H, int64_t W, int sr, int mode, int64_t* mv,
                                   hipStream_t s) {
@@ -992,45 +699,29 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
   me_generic_kernel<T, M><<<grid, 256, 0, s>>>((const T*)ref, (const T*)cur, nframes, h, w, sr, mv)
   if (mode == IVC_ME_EXACT_U8) {
     if (dtype != IVC_U8) return hipErrorInvalidValue;
-    // the dot4 searches address a frame's S2 plane (4 B per pixel) with 32-bit buffer offsets
-    // the matrix-core +-16 search needs no S2 plane: the whole batch in one launch
-    if (IVC_ME_TILE && sr == 16 && me_use_mfma() && launch_me_mfma16((const uint8_t*)ref, (const uint8_t*)cur,
-                                                                     nframes, h, w, mv, s))
+    // +-16: the matrix-core search (no S2 plane; the whole batch, chunked by the launcher)
+    if (sr == 16 && launch_me_mfma16((const uint8_t*)ref, (const uint8_t*)cur, nframes, h, w, mv, s))
       return hipGetLastError();
-    if ((sr == 4 || sr == 8 || sr == 16) && H * W * 4 < ((int64_t)1 << 31)) {
+    // +-4 / +-8: the dot4 search; it addresses a frame's S2 plane (4 B per pixel) with 32-bit
+    // buffer offsets
+    if ((sr == 4 || sr == 8) && H * W * 4 < ((int64_t)1 << 31)) {
       // Frame pairs go in chunks of about IVC_ME_CHUNK_BYTES of S2 (one int32 per reference
       // pixel, stream-ordered scratch; at least one frame): a chunk the size of the 256 MB
       // Infinity Cache is still cache-resident when the search reads it right after the
-      // pre-pass wrote it.  Same-process A/B against one whole-batch S2: 1080p x 300 inter
-      // 16.6 -> 14.5 ms, 8K x 120 134.7 -> 94.0 ms; 128 MB / 64 MB chunks are slower at 1080p
-      // (more, smaller launches)
+      // pre-pass wrote it
       const int64_t hw = H * W;
       int64_t chunk = (int64_t)IVC_ME_CHUNK_BYTES / (4 * hw);
       if (chunk < 1) chunk = 1;
       if (chunk > nframes) chunk = nframes;
       int32_t* s2 = me_s2_alloc(chunk * hw, s);
       if (!s2) return hipErrorOutOfMemory;
-      const bool tiled = IVC_ME_TILE && sr == 16;
-      // the tiled search reads S2 words of masked candidates too: clear the positions the
-      // pre-pass never writes (x > W-8, y > H-8) once, so every word read is bounded
-      if (tiled) {
-        const hipError_t e = hipMemsetAsync(s2, 0, (size_t)(chunk * hw) * 4, s);
-        if (e != hipSuccess) return e;
-      }
       for (int64_t f0 = 0; f0 < nframes; f0 += chunk) {
         const int64_t nf = nframes - f0 < chunk ? nframes - f0 : chunk;
         const uint8_t* rf = (const uint8_t*)ref + f0 * hw;
         const uint8_t* cf = (const uint8_t*)cur + f0 * hw;
         int64_t* mf = mv + f0 * (H / 8) * (W / 8);
         const unsigned s2grid = me_grid(nf * ((W - 8) / 4 + 1) * ((H - 8) / S2Y + 1), 256, 8);
-        if (tiled) {
-          me_s2_kernel<true><<<s2grid, 256, 0, s>>>(rf, nf, h, w, s2);
-          const int64_t tiles = nf * (H / 8) * ((W / 8 + ts::TB - 1) / ts::TB);
-          me_tile16_kernel<<<me_fast_grid(reinterpret_cast<const void*>(me_tile16_kernel), tiles),
-                             256, 0, s>>>(rf, cf, s2, nf, h, w, mf);
-          continue;
-        }
-        me_s2_kernel<false><<<s2grid, 256, 0, s>>>(rf, nf, h, w, s2);
+        me_s2_kernel<<<s2grid, 256, 0, s>>>(rf, nf, h, w, s2);
         // persistent (group stride = all waves), launched at 2x what fits at once: the waves
         // of the second residency round fill the SIMDs as the first ones drain (measured
         // faster than an exactly resident grid, the kernel being VALU-throughput bound)
@@ -1039,11 +730,8 @@ hipError_t launch_motion_estimate(const void* ref, const void* cur, int dtype, i
   me_fast_u8_kernel<R><<<me_fast_grid(reinterpret_cast<const void*>(me_fast_u8_kernel<R>),      \
                                       ((groups_bpw1 + BPW - 1) / BPW + 3) / 4),                 \
                          256, 0, s>>>(rf, cf, s2, nf, h, w, mf)
-        switch (sr) {
-          case 4: ME_FAST(4, 4); break;
-          case 8: ME_FAST(8, 2); break;
-          default: ME_FAST(16, 1); break;
-        }
+        if (sr == 4) ME_FAST(4, 4);
+        else ME_FAST(8, 2);
 #undef ME_FAST
       }
       (void)hipFreeAsync(s2, s);

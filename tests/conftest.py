@@ -13,6 +13,21 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) and the built libivc.so")
 
 
+@pytest.fixture
+def tune():
+    """tune(name, value): an ivc_set_tuning override (chunk counts, the symbols -> image
+    fallback) for this test only; every key it touched is restored at teardown."""
+    from ivclab_amd import _native as N
+    saved = {}
+
+    def set_(name, value):
+        prev = N.set_tuning(name, value)
+        saved.setdefault(name, prev)
+    yield set_
+    for name, prev in saved.items():
+        N.set_tuning(name, prev)
+
+
 @pytest.fixture(scope="session")
 def golden():
     import numpy as np

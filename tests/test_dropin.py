@@ -83,14 +83,20 @@ for mod, name in (('ivclab.signal', 'downsample'), ('ivclab.signal', 'FilterPipe
                   ('ivclab.image', 'IntraCodecAdaptive'), ('ivclab.entropy', 'stats_joint')):
     try:
         exec(f'from {mod} import {name}')
-    except ImportError:
-        pass
+    except ImportError as e:                 # the reason reaches the from-import form too
+        assert 'outside the MI355X block-codec hot path' in str(e), (name, str(e))
     else:
         raise AssertionError(name)
 try:
     ivclab.signal.downsample
-except AttributeError as e:
+except ImportError as e:
     assert 'outside the MI355X block-codec hot path' in str(e)
+else:
+    raise AssertionError('downsample')
+try:
+    ivclab.signal.no_such_name
+except AttributeError as e:
+    assert 'outside' not in str(e)
 print('ok')
 """)
     assert out.strip() == "ok"

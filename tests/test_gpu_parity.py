@@ -80,6 +80,8 @@ def test_host_pipeline_chunking_changes_nothing():
     pq, zz, pt = PatchQuant(0.7), ZigZag(), Patcher()
     L = N.lib()
     outs = []
+    prev = int(L.ivc_host_pipeline())
+    assert prev == 0, "the library default runs host-buffer calls in one piece"
     try:
         for chunk in (0, 1 << 20, 3 << 20, 8 << 20):
             N.check(L.ivc_set_host_pipeline(chunk))
@@ -88,7 +90,8 @@ def test_host_pipeline_chunking_changes_nothing():
             z = zz.flatten(q)
             outs.append((d, q, z, pq.dequantize(q), zz.unflatten(z)))
     finally:
-        N.check(L.ivc_set_host_pipeline(8 << 20))
+        N.check(L.ivc_set_host_pipeline(prev))
+    assert int(L.ivc_host_pipeline()) == prev
     for o in outs[1:]:
         for a, b in zip(o, outs[0]):
             assert_bits(a, b, "pipelined vs one piece")
@@ -981,7 +984,7 @@ def test_zerorun_device_wide_and_general(nblk):
 
 @pytest.mark.parametrize("chunks", [None, 5])
 @pytest.mark.parametrize("tier", ["int8", "some_int16", "int32_value", "int16_slots_full"])
-def test_zerorun_int8_handoff_tiers(tier, chunks, monkeypatch):
+def test_zerorun_int8_handoff_tiers(tier, chunks, tune):
     """The dense-row encoder hands the coefficients from its count pass to its emission pass
     as int8, a group with a value outside int8 as int16 (side slots for 1 in 8 groups), and
     falls back to emitting from the int32 rows when a value lies outside int16 or the int16
@@ -990,7 +993,7 @@ def test_zerorun_int8_handoff_tiers(tier, chunks, monkeypatch):
     torch = pytest.importorskip("torch")
     import ivclab_amd.device as D
     if chunks:     # the pipelined call (count of chunk j + 1 beside the emission of chunk j)
-        monkeypatch.setenv("IVC_ZR_FORCE_CHUNKS", str(chunks))
+        tune("zr_chunks", chunks)
     nblk = 16 * 2000 + 3
     rng = np.random.default_rng(hash(tier) % 1000)
     x = rng.integers(-100, 101, (nblk, 64)).astype(np.int32)
@@ -1212,15 +1215,15 @@ def test_intra_symbols_emission_histogram(case):
 
 @pytest.mark.parametrize("case,chunks", [("s1", 2), ("s1", 5), ("s007", 3), ("s0005", 2),
                                         ("rgb", 4), ("ragged", 5), ("odd_rows", 3)])
-def test_intra_symbols_pipelined_chunks(monkeypatch, case, chunks):
+def test_intra_symbols_pipelined_chunks(tune, case, chunks):
     """The count pass and the emitter pipelined over chunks of whole frames
-    (IVC_SYM_FORCE_CHUNKS; the bench's 256 x 4K call takes 16): stream, length and emission
+    (the sym_chunks override; the bench's 256 x 4K call takes 16): stream, length and emission
     histogram equal the oracle's for every hand-off tier (s007: int16 slots; s0005: the
     emitters stand down and the fused emission pass runs over every frame), a capacity-cut
     stream, and a frame whose group count is not a multiple of 4 (odd_rows: one chunk)."""
     torch = pytest.importorskip("torch")
     import ivclab_amd.device as D
-    monkeypatch.setenv("IVC_SYM_FORCE_CHUNKS", str(chunks))
+    tune("sym_chunks", chunks)
     rng = np.random.default_rng(chunks * 31 + len(case))
     F, H, W, C = 5, 48, 128, 1
     scale = {"s007": 0.07, "s0005": 0.0005}.get(case, 1.0)
@@ -1249,6 +1252,37 @@ def test_intra_symbols_pipelined_chunks(monkeypatch, case, chunks):
     torch.cuda.synchronize()
     assert int(nsym.item()) == want.size
     assert np.array_equal(cut.cpu().numpy(), want[:want.size // 3])
+
+
+@pytest.mark.parametrize("chunks", [2, 5])
+def test_intra_symbols_pipelined_late_int16_overflow(tune, chunks):
+    """Only the LAST frame holds a coefficient outside int16, so only the last chunk's count pass
+    sets the stand-down word: the emitters of the earlier chunks may already have run (and
+    counted their symbols) when it is set.  The emission histogram must still count every symbol
+    exactly once (the emitters' counts join the caller's histogram only when no chunk stood
+    down), and the stream must equal the oracle's."""
+    torch = pytest.importorskip("torch")
+    import ivclab_amd.device as D
+    tune("sym_chunks", chunks)
+    rng = np.random.default_rng(chunks)
+    F, H, W = 5, 48, 128
+    img = rng.integers(0, 3, (F, H, W, 1), dtype=np.uint8)       # dim frames: |coef| <= int16
+    img[-1] = rng.integers(0, 256, (H, W, 1), dtype=np.uint8)    # the bright last frame
+    table = PatchQuant(0.0005).get_quantization_table().astype(np.float64)
+    peak = [np.abs(np.round(O.dct_transform(O.patch(img[f])) / table[None, None])).max() for f in range(F)]
+    assert max(peak[:-1]) <= 32767 < peak[-1], peak
+    want = _zr_chain(img, table)
+    fr = torch.from_numpy(img[..., 0]).cuda()
+    nsym = torch.zeros(1, dtype=torch.int64, device="cuda")
+    out = torch.full((want.size,), -1, dtype=torch.int32, device="cuda")
+    ref = O.histogram(want, -4097, 8194)
+    for rep in range(3):
+        hist = torch.zeros(8194, dtype=torch.int64, device="cuda")
+        D.intra_symbols(fr, table, out, nsym, hist=hist, hist_lo=-4097)
+        torch.cuda.synchronize()
+        assert int(nsym.item()) == want.size
+        assert_bits(out.cpu().numpy(), want, (chunks, rep))
+        assert np.array_equal(hist.cpu().numpy(), ref), (chunks, rep)
 
 
 @pytest.mark.parametrize("shift", [1, 2, 3])

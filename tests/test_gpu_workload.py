@@ -1,8 +1,8 @@
 """Parity of the exact chains bench.py times, at (or past) their workload sizes.
 
-bench.py's legs run code paths the small parity tests never reach: the fast exact-u8 motion
-search over many frame pairs in 256 MB S2 chunks (32 pairs per chunk at 1080p) feeding the
-SRC_INTER residual DCT + quantiser (cfg4), the fused intra kernel writing a batch whose
+bench.py's legs run code paths the small parity tests never reach: the matrix-core exact-u8
++-16 motion search over many frame pairs feeding the SRC_INTER residual DCT + quantiser (cfg4,
+in one piece and pipelined over chunks of pairs), the fused intra kernel writing a batch whose
 output lies past 4 GiB (cfg3), and the chunked cfg5 step with its side-stream histograms.
 These tests run those chains on the bench's own synthetic generators and compare sampled
 frames (whole frames, every block) with the C/NumPy oracle (oracle.c_inter_encode:
@@ -32,11 +32,14 @@ def assert_bits(a, b, what=""):
         raise AssertionError(f"{what}: {bad.size} differing elements, first at {bad[0]}")
 
 
-def test_inter_encode_sr16_1080p_across_s2_chunks():
+@pytest.mark.parametrize("chunks", [0, 3])
+def test_inter_encode_sr16_1080p_across_s2_chunks(tune, chunks):
     """cfg4's chain at its frame size: 40 frames of the bench's 1080p sequence at sr = 16
-    (the fast dot4 search; 39 pairs = two S2 chunks of 32 + 7).  Pairs 0, 31 (last of chunk
-    0), 32 (first of chunk 1) and 38 (last) are checked whole — every motion vector and every
-    quantised residual coefficient — against the C oracle chain."""
+    (me_mfma16x2_kernel then the residual encoder), in one piece and pipelined over 3 chunks of
+    pairs (the inter_chunks override: the search of chunk j + 1 beside the residual encode of
+    chunk j on the second stream).  Pairs 0, 31, 32 and 38 are checked whole — every motion
+    vector and every quantised residual coefficient — against the C oracle chain."""
+    tune("inter_chunks", chunks)
     dev = torch.device("cuda:0")
     F, H, W, sr = 40, 1080, 1920, 16
     seq = bench.inter_frames(F, H, W, seed=4, dev=dev)
@@ -55,18 +58,14 @@ def test_inter_encode_sr16_1080p_across_s2_chunks():
 
 
 def test_inter_encode_sr16_8k_chunks():
-    """cfg5's chain at its own frame size (BASELINE configs[4], 7680x4320): one 8K S2 plane is
-    132.7 MB, so the 256 MiB S2 chunk holds TWO frame pairs (at 1080p it holds 32) and the
-    search loop alternates pre-pass and tiled search every two pairs (ivc_motion.hip
-    launch_motion_estimate).  4 frames of the bench's cfg5 sequence (3 pairs = a full chunk of
-    2 and a remainder chunk of 1): mv and q of the top, middle and bottom
+    """cfg5's chain at its own frame size (BASELINE configs[4], 7680x4320): 4 frames of the
+    bench's cfg5 sequence (3 pairs): mv and q of the top, middle and bottom
     block-row stripes of every pair against the C oracle chain (motion.py:8-58,
     patchquant.py:44-60); every pair written; and the chunked side-stream histograms of the
     cfg5 step (1 pair per chunk) equal one call followed by main-stream histograms."""
     import ivclab_amd._native as N
     dev = torch.device("cuda:0")
     F, H, W, sr = 4, 4320, 7680, 16
-    assert (256 << 20) // (H * W * 4) == 2              # pairs per S2 chunk at 8K
     seq = bench.inter_frames(F, H, W, seed=5, dev=dev)
     P, h = F - 1, H // 8
     nmv = (2 * sr + 1) ** 2
@@ -239,18 +238,18 @@ def test_chunked_inter_encode_with_side_stream_histograms():
 
 
 @pytest.mark.parametrize("C,chunks", [(3, None), (1, None), (3, 3), (1, 16)])
-def test_symbols2image_fused_adversarial(monkeypatch, C, chunks):
+def test_symbols2image_fused_adversarial(tune, C, chunks):
     """The fused symbols -> image kernel (ivc_decode.hip sym_image_kernel: zero-run expansion
     into LDS, dequantise, IDCT, unpatch, ycbcr2rgb; intracodec.py:84-146 + zerorun.py:44-88)
-    alone — IVC_S2I_NO_FALLBACK=1 keeps the general decoder from overwriting its image — on
+    alone — the s2i_no_fallback override keeps the general decoder from overwriting its image — on
     coefficients built to stress it: all-zero blocks (one EOB per block-plane, so 4096-symbol
     tiles hold dozens of group starts), densest blocks (value, 0, run 1, ... = 97 symbols per
     block-plane), long runs, a value at zig-zag position 63, large DCs, a ragged last group
     (w = 125 block columns) and a stream of 130k-380k symbols over 30-90 tiles; against the
     oracle chain (ZeroRunCoder.decode, unflatten, dequantise, IDCT, unpatch, ycbcr2rgb)."""
-    monkeypatch.setenv("IVC_S2I_NO_FALLBACK", "1")
+    tune("s2i_no_fallback", 1)
     if chunks:     # the pipelined call (ivc_entropy.hip s2i_pipelined) on a stream of 30-90 tiles
-        monkeypatch.setenv("IVC_S2I_FORCE_CHUNKS", str(chunks))
+        tune("s2i_chunks", chunks)
     dev = torch.device("cuda:0")
     rng = np.random.default_rng(40 + C)
     F, H, W = 2, 128, 1000
@@ -280,10 +279,10 @@ def test_symbols2image_fused_adversarial(monkeypatch, C, chunks):
 
 
 @pytest.mark.parametrize("chunks", [1, 4, 13])
-def test_symbols2image_pipelined_rejects_and_falls_back(monkeypatch, chunks):
+def test_symbols2image_pipelined_rejects_and_falls_back(tune, chunks):
     """A malformed block (a run past 64 coefficients) in the middle of a 40-tile stream: the
     fused path — one pass or pipelined over chunks of tiles — rejects the stream
-    (IVC_S2I_NO_FALLBACK reports IVC_S2I_REJECTED), and with the fallback the call reports the
+    (the s2i_no_fallback override reports err[0] = -100), and with the fallback the call reports the
     reference's error, as ZeroRunCoder.decode raises it (zerorun.py:66-70)."""
     from ivclab_amd.image import IntraCodec
     dev = torch.device("cuda:0")
@@ -296,7 +295,7 @@ def test_symbols2image_pipelined_rejects_and_falls_back(monkeypatch, chunks):
     cut = eobs[len(eobs) // 2] + 1                     # a block boundary mid-stream
     bad = np.concatenate([sym[:cut], [0, 70], sym[cut:]]).astype(np.int32)
     table = PatchQuant(1.0).get_quantization_table()
-    monkeypatch.setenv("IVC_S2I_FORCE_CHUNKS", str(chunks))
+    tune("s2i_chunks", chunks)
     out = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
     err = torch.full((3,), -1, dtype=torch.int64, device=dev)
     # the clean stream decodes identically whatever the chunking
@@ -305,11 +304,11 @@ def test_symbols2image_pipelined_rejects_and_falls_back(monkeypatch, chunks):
     assert err.tolist() == [0, 0, 0]
     want0 = O.ycbcr2rgb(O.unpatch(O.intra_decode(q[0], 1.0, unzigzag=True)))
     assert_bits(out[0].cpu().numpy(), want0, f"clean stream, chunks={chunks}")
-    monkeypatch.setenv("IVC_S2I_NO_FALLBACK", "1")
+    tune("s2i_no_fallback", 1)
     D.symbols2image(torch.from_numpy(bad).to(dev), C, table, out, err, to_rgb=True)
     torch.cuda.synchronize()
     assert int(err[0]) == -100, err.tolist()
-    monkeypatch.delenv("IVC_S2I_NO_FALLBACK")
+    tune("s2i_no_fallback", 0)
     codec = IntraCodec(quantization_scale=1.0)
     with pytest.raises(Exception) as got:
         codec.symbols2image(bad, (H, W, 3))
