@@ -554,8 +554,8 @@ double ivc_store_pace(void) { return store_pace_gbps(); }
 double ivc_store_pace_late(void) { return store_pace_late_fraction(); }
 
 int ivc_store_pace_stats(int encoder, double* out, int n) {
-  if (encoder < 0 || encoder > 2 || n < 0 || (n > 0 && !out))
-    return fail(IVC_E_ARG, "ivc_store_pace_stats: encoder must be 0, 1 or 2, out must hold n values");
+  if (encoder < 0 || encoder > 3 || n < 0 || (n > 0 && !out))
+    return fail(IVC_E_ARG, "ivc_store_pace_stats: encoder must be 0..3, out must hold n values");
   return store_pace_stats(encoder, out, n);
 }
 
@@ -565,8 +565,8 @@ int ivc_store_pace_reset_stats(void) {
 }
 
 int ivc_store_pace_trace(int encoder, double* out, int max_records) {
-  if (encoder < 0 || encoder > 2 || max_records < 0 || (max_records > 0 && !out))
-    return fail(IVC_E_ARG, "ivc_store_pace_trace: encoder must be 0, 1 or 2, out must hold "
+  if (encoder < 0 || encoder > 3 || max_records < 0 || (max_records > 0 && !out))
+    return fail(IVC_E_ARG, "ivc_store_pace_trace: encoder must be 0..3, out must hold "
                            "7 * max_records values");
   return store_pace_trace(encoder, out, max_records);
 }

@@ -423,6 +423,9 @@ struct FusedArgs {
 #ifndef IVC_WIDE_NG
 #define IVC_WIDE_NG 2    // u8 luma: 8 rows x 128 bytes per wave load (whole cache lines)
 #endif
+#ifndef IVC_C3_PLANE_STORE
+#define IVC_C3_PLANE_STORE 1   // C = 3 coefficients: each plane stored as soon as it is quantised
+#endif
 
 constexpr int XS_PITCH = 72;   // T elements per block in the transpose image
 // int32 per block in the output staging: 3 planes (192 + 8 pad), or 2 planes (128 + 8) when
@@ -431,11 +434,15 @@ template <int C, bool DUP>
 constexpr int os_pitch() { return C == 1 && DUP ? 136 : 200; }
 constexpr int OOB = 0x40000000;  // buffer offset beyond every descriptor range used here
 
-template <typename T, int C, bool DUP>
+// C = 3 plane-store mode (PST): one plane staged at a time, block pitch 72 int32 (= 8 mod 32,
+// like 136 and 200: the quantiser's writes stay conflict-free), aliasing the transpose image
+constexpr int PST_PITCH = 72;
+template <typename T, int C, bool DUP, bool PST = false>
 struct WaveLds {
   static constexpr int XS = 8 * XS_PITCH * (int)sizeof(T);
-  static constexpr int OS = 8 * os_pitch<C, DUP>() * 4;
-  static constexpr int BYTES = C == 1 ? (XS > OS ? XS : OS) : XS + OS;  // C = 1 aliases them
+  static constexpr int OS = 8 * (PST ? PST_PITCH : os_pitch<C, DUP>()) * 4;
+  // C = 1 and the plane-store mode alias them (the quantiser writes after the transpose reads)
+  static constexpr int BYTES = (C == 1 || PST) ? (XS > OS ? XS : OS) : XS + OS;
 };
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
@@ -666,6 +673,25 @@ __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* o
   }
 }
 
+// Plane p of the staged group (PST: block pitch PST_PITCH) leaves as 2 x 1 KiB
+// buffer_store_dwordx4: block bb's 256 bytes at byte (bb * 192 + p * 64) * 4 of the group.
+template <int NG>
+__device__ __forceinline__ void store_plane(const FusedArgs& a, const int32_t* os, int lane,
+                                            uint32_t lt, int g, int p, bool exists) {
+  const GroupLoc L = group_loc<NG>(a, lt, g);
+  const __amdgpu_buffer_rsrc_t ro =
+      make_rsrc(a.out + (((int64_t)L.f * a.h + L.bi) * a.w + L.bj0) * 192 + p * 64,
+                exists && L.nb > 0 ? (uint32_t)(L.nb - 1) * 768u + 256u : 0u);
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj) {
+    const int ch = lane + 64 * jj;
+    const int bb = ch >> 4, cc = ch & 15;
+    const int4 val = *reinterpret_cast<const int4*>(os + bb * PST_PITCH + cc * 4);
+    const u32x4 w4 = {(uint32_t)val.x, (uint32_t)val.y, (uint32_t)val.z, (uint32_t)val.w};
+    __builtin_amdgcn_raw_buffer_store_b128(w4, ro, bb * 768 + cc * 16, 0, IVC_STORE_AUX);
+  }
+}
+
 // Output modes of the fused kernel: the quantised blocks themselves (OUT_COEFS: staged in LDS
 // and stored), or the blocks' zero-run symbols (ivclab/entropy/zerorun.py:10-43) — their
 // per-group counts (OUT_COUNT) or the symbol stream at scanned offsets (OUT_SYMBOLS).
@@ -678,11 +704,17 @@ __device__ __forceinline__ void store_group(const FusedArgs& a, const int32_t* o
 enum { OUT_COEFS = 0, OUT_COUNT = 1, OUT_SYMBOLS = 2, OUT_LUMA = 3, OUT_SYMH = 4, OUT_COEFH = 5 };
 
 // Transform + quantise one group (lane (b, r)) from its raw rows into the LDS staging.
+// PST (C = 3 coefficients): plane c is staged alone at os (aliasing xs) and handed to
+// plane_done(c) right after its quantisation, before plane c + 1 reuses the region.
+struct NoPlaneDone {
+  __device__ __forceinline__ void operator()(int) const {}
+};
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
-          bool DUP, bool LUMA = false>
+          bool DUP, bool LUMA = false, bool PST = false, typename PlaneDone = NoPlaneDone>
 __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI, C, SRC>& v,
                                              T* xs, int32_t* os, const double* srq, const D* sq,
-                                             int b, int r, uint32_t zp0, uint32_t zp1) {
+                                             int b, int r, uint32_t zp0, uint32_t zp1,
+                                             PlaneDone plane_done = NoPlaneDone{}) {
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     // ---- row pass (axis -1): lane owns row r of block b ------------------------------------
@@ -734,7 +766,7 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
       if (C == 1 && DUP && pi == 2) break;  // plane 2 == plane 1: stored from plane 1
       if (LUMA && pi > 0) break;
       const int p = C == 1 ? pi : c;
-      int32_t* ob = os + b * os_pitch<C, DUP>() + p * 64;
+      int32_t* ob = PST ? os + b * PST_PITCH : os + b * os_pitch<C, DUP>() + p * 64;
       auto pos_of = [&](int i) {
         return ZZ ? (int)(((i < 4 ? zp0 : zp1) >> (8 * (i & 3))) & 63u) : i * 8 + r;
       };
@@ -776,6 +808,10 @@ __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI
       }
     }
     __builtin_amdgcn_wave_barrier();
+    if constexpr (PST) {
+      plane_done(c);
+      __builtin_amdgcn_wave_barrier();
+    }
   }
 }
 
@@ -1251,7 +1287,10 @@ __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && 
   static_assert(OUTM != OUT_LUMA || C == 1, "the luma-only output is for C = 1 images");
   constexpr bool COEF = OUTM == OUT_COEFS || OUTM == OUT_LUMA || OUTM == OUT_COEFH;
   constexpr bool SYM = OUTM == OUT_SYMBOLS || OUTM == OUT_SYMH;   // emission pass
-  typedef WaveLds<T, C, DUP> L;
+  // C = 3 coefficients: each plane stored as soon as it is quantised, so one plane is staged and
+  // the staging aliases the transpose image (21.5 KB of LDS per workgroup instead of 47 KB)
+  constexpr bool PST = IVC_C3_PLANE_STORE && C == 3 && OUTM == OUT_COEFS;
+  typedef WaveLds<T, C, DUP, PST> L;
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
   __shared__ double srq[FAST ? 192 : 1];
   __shared__ D sq[192];
@@ -1289,7 +1328,7 @@ __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && 
 
   unsigned char* mine = lds + wave * L::BYTES;
   T* xs = reinterpret_cast<T*>(mine);
-  int32_t* os = reinterpret_cast<int32_t*>(mine + (C == 1 ? 0 : L::XS));
+  int32_t* os = reinterpret_cast<int32_t*>(mine + ((C == 1 || PST) ? 0 : L::XS));
   const uint32_t nlt = a.nframes * (uint32_t)(a.h * a.tpr);
   const uint32_t nwaves = gridDim.x * 4u;
   uint32_t lt = blockIdx.x * 4u + wave;
@@ -1306,19 +1345,21 @@ __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && 
   // late slots of the wave's first PACE_EARLY slots (start-up: the grid is still being
   // dispatched and the first tiles loaded while the schedule runs) and of the rest
   uint32_t nlate_early = 0, nlate = 0, pslot = 0, first_late = 0xffffffffu;
+  // the pacing wait of the next slot (PST: before a group's first plane store)
+  auto pace_slot = [&]() {
+    const uint32_t l = pace_until(pace_next, a.pace_d);
+    if (pslot < a.pace_early) {
+      nlate_early += l;
+    } else {
+      nlate += l;
+      if (l && first_late == 0xffffffffu) first_late = pslot;
+    }
+    ++pslot;
+    pace_next += a.pace_d;
+  };
   auto store_prev = [&](uint32_t plt, int pg, bool have_prev) {
-    if constexpr (COEF) {
-      if (a.pace_d && have_prev) {
-        const uint32_t l = pace_until(pace_next, a.pace_d);
-        if (pslot < a.pace_early) {
-          nlate_early += l;
-        } else {
-          nlate += l;
-          if (l && first_late == 0xffffffffu) first_late = pslot;
-        }
-        ++pslot;
-        pace_next += a.pace_d;
-      }
+    if constexpr (COEF && !PST) {
+      if (a.pace_d && have_prev) pace_slot();
       store_group<NG, C, DUP, OUTM == OUT_LUMA>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
     }
   };
@@ -1358,7 +1399,13 @@ __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && 
           store_prev(plt, pg, have_prev);
           RowReg<TI, C, SRC> v;
           group_row<TI, C, NG>(ring[p], g, lane, v);
-          encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+          encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA, PST>(
+              a, v, xs, os, srq, sq, b, r, zp0, zp1, [&](int c) {
+                if constexpr (PST) {
+                  if (c == 0 && a.pace_d && ex) pace_slot();
+                  store_plane<NG>(a, os, lane, tp, g, c, ex && !IVC_SKIP(a, 16));
+                }
+              });
           if constexpr (OUTM == OUT_COEFH) {
             if (ex) coef_hist<C, DUP>(a, os, group_loc<NG>(a, tp, g).nb, hacc.bins);
           }
@@ -1402,7 +1449,13 @@ __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && 
         } else {
           gather_inter(a, lt, b, r, v);
         }
-        encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA>(a, v, xs, os, srq, sq, b, r, zp0, zp1);
+        encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, OUTM == OUT_LUMA, PST>(
+            a, v, xs, os, srq, sq, b, r, zp0, zp1, [&](int c) {
+              if constexpr (PST) {
+                if (c == 0 && a.pace_d) pace_slot();
+                store_plane<NG>(a, os, lane, lt, g, c, !IVC_SKIP(a, 16));
+              }
+            });
         if constexpr (OUTM == OUT_COEFH) coef_hist<C, DUP>(a, os, group_loc<NG>(a, lt, g).nb, hacc.bins);
         if constexpr (!COEF)
           zr_group<C, DUP, OUTM>(a, os, b, r, group_loc<NG>(a, lt, g).nb, (int64_t)lt * NG + g, hacc);
@@ -1414,16 +1467,10 @@ __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && 
     }
   }
   if constexpr (COEF) {
-    if (a.pace_d && have_prev) {
-      const uint32_t l = pace_until(pace_next, a.pace_d);
-      if (pslot < a.pace_early) {
-        nlate_early += l;
-      } else {
-        nlate += l;
-        if (l && first_late == 0xffffffffu) first_late = pslot;
-      }
+    if constexpr (!PST) {
+      if (a.pace_d && have_prev) pace_slot();
+      store_group<NG, C, DUP, OUTM == OUT_LUMA>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
     }
-    store_group<NG, C, DUP, OUTM == OUT_LUMA>(a, os, lane, plt, pg, have_prev && !IVC_SKIP(a, 16));
     if ((nlate | nlate_early) && lane == 0) {
       unsigned long long* blk = reinterpret_cast<unsigned long long*>(a.pace_t0);
       __hip_atomic_fetch_add(blk + 1 + blockIdx.x % PACE_SHARDS,
@@ -1572,7 +1619,7 @@ struct PaceState {
   int64_t gen = 0;                // bumped by ivc_set_store_pace: older launches are not folded
 };
 // per device and per encoder (0: image source, 1: inter residual source, 2: luma-only image)
-static PaceState g_pace[64][3];
+static PaceState g_pace[64][4];
 
 static double pace_start_rate() {
   if (g_pace_start < 0) {
@@ -1857,8 +1904,9 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
   const double out_bytes = OUTM == OUT_LUMA ? 256.0 : 768.0;
   const double gbytes = 8.0 * (SRC == SRC_INTER ? 64.0 * 2 + 8.0 + out_bytes
                                                 : 64.0 * C * sizeof(TI) + out_bytes);
-  // pacing state per encoder: image source, inter residual, luma-only image
-  const int kind = OUTM == OUT_LUMA ? 2 : SRC;
+  // pacing state per encoder: image source, inter residual, luma-only image, 3-channel image
+  // (each adapts its own rate: a 3-channel launch runs at a different pace than a luma one)
+  const int kind = OUTM == OUT_LUMA ? 2 : (C == 3 && SRC == SRC_IMAGE ? 3 : SRC);
   auto go = [&](auto k) {
     const unsigned g = grid(k);
     const int64_t nw = 4 * (int64_t)g;

@@ -48,6 +48,9 @@ constexpr int MASK_C = -(1 << 22);               // C of a (block, window) pair 
 
 typedef int mf_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned int mf_u32x2 __attribute__((ext_vector_type(2)));
+#ifndef IVC_ME_PAIR
+#define IVC_ME_PAIR 1
+#endif
 
 // ---- two block rows per tile --------------------------------------------------
 // A tile is 8 adjacent blocks of block row by (top) and the 8 below them (bottom): 16 MFMA
@@ -136,12 +139,102 @@ __device__ __forceinline__ void me2_search(const uint32_t* lds, int* red, int wa
       if (bot && q23) acc[3] = max(acc[3], (int)(((uint32_t)d.w << 8) + e));
     }
   };
+  // IVC_ME_PAIR: the two M-tiles of a segment as two independent MFMA chains interleaved step
+  // by step (each step's row and energy reads issued a step ahead), so one chain's MFMA covers
+  // the other's result latency and the keys of both fold into one v_max3 per register.  The
+  // steps go in a rolled loop of step pairs (even offset: block operand bop, odd: bks) — fully
+  // unrolled, the scheduler's hoisting spills
+  auto mpair = [&](int mt0, auto q01c, auto q23c) {
+    constexpr bool q01 = decltype(q01c)::value, q23 = decltype(q23c)::value;
+    // (opaque to the optimiser: what derives from mt0 — masks, addresses — is then formed here,
+    // not hoisted out of the tile loop to stay live through the staging and energy phases)
+    asm volatile("" : "+s"(mt0));
+    const int wd = 4 * mt0 + (l16 >> 2);
+    const int v0 = 16 * mt0 + l16 - 8 * g, v1 = v0 - 32, v2 = v0 + 16, v3 = v1 + 16;
+    const int c0 = (unsigned)v0 <= 32u ? 0 : MASK_C, c1 = (unsigned)v1 <= 32u ? 0 : MASK_C;
+    const int c2 = (unsigned)v2 <= 32u ? 0 : MASK_C, c3 = (unsigned)v3 <= 32u ? 0 : MASK_C;
+    const mf_v4i cmA = mf_v4i{c0, c1, c0, c1}, cmB = mf_v4i{c2, c3, c2, c3};
+    const uint32_t* rb = cb + (r0 + 2 * g) * PITCH + wd;   // row kk: rb + kk * PITCH
+    const int* em = ev + 16 * mt0;                          // offset dl: em + dl * U
+    mf_v4i TA, TB;
+    TA = mf_v4i{(int)rb[0], (int)rb[1], (int)rb[PITCH], (int)rb[PITCH + 1]};
+    TB = mf_v4i{(int)rb[4], (int)rb[5], (int)rb[PITCH + 4], (int)rb[PITCH + 5]};
+    int eA = em[0], eB = em[16];
+    // one step at offset dl (ODD: dl odd); `more`: a step follows (its row and energies are read)
+    auto step = [&](int dl, auto oddc, auto topc, auto botc, bool more) {
+      constexpr bool ODD = decltype(oddc)::value;
+      constexpr bool top = decltype(topc)::value, bot = decltype(botc)::value;
+      mf_u32x2 nA = {0u, 0u}, nB = {0u, 0u};
+      int neA = 0, neB = 0;
+      if (more) {
+        const uint32_t* p = rb + (dl + 2) * PITCH;
+        nA = mf_u32x2{p[0], p[1]};
+        nB = mf_u32x2{p[4], p[5]};
+        neA = em[(dl + 1) * U];
+        neB = em[(dl + 1) * U + 16];
+      }
+      const mf_v4i bo = ODD ? bks : bop;
+      const mf_v4i dA = __builtin_amdgcn_mfma_i32_16x16x64_i8(bo, TA, cmA, 0, 0, 0);
+      const mf_v4i dB = __builtin_amdgcn_mfma_i32_16x16x64_i8(bo, TB, cmB, 0, 0, 0);
+      const uint32_t ea = (uint32_t)eA, eb = (uint32_t)eB;
+      auto k2 = [&](int i, int x, int y) {
+        acc[i] = max(acc[i], max((int)(((uint32_t)x << 8) + ea), (int)(((uint32_t)y << 8) + eb)));
+      };
+      if (top && q01) k2(0, dA.x, dB.x);
+      if (top && q23) k2(1, dA.y, dB.y);
+      if (bot && q01) k2(2, dA.z, dB.z);
+      if (bot && q23) k2(3, dA.w, dB.w);
+      // the next step uses rows (dl + 1, dl + 2): row dl + 2 replaces row dl's half
+      if (ODD) {
+        TA.z = (int)nA.x; TA.w = (int)nA.y;
+        TB.z = (int)nB.x; TB.w = (int)nB.y;
+      } else {
+        TA.x = (int)nA.x; TA.y = (int)nA.y;
+        TB.x = (int)nB.x; TB.y = (int)nB.y;
+      }
+      eA = neA;
+      eB = neB;
+    };
+    using T_ = std::true_type;
+    using F_ = std::false_type;
+    // R = r0 + dl: top blocks live for R <= 32, bottom for R >= 8
+    if constexpr (WV == 0) {          // R 0..10: bottom from dl = 8
 #pragma unroll 1
-  for (int mt = 0; mt < 2; ++mt) mtile(mt, std::true_type{}, std::false_type{});
+      for (int dl = 0; dl < 8; dl += 2) {
+        step(dl, F_{}, T_{}, F_{}, true);
+        step(dl + 1, T_{}, T_{}, F_{}, true);
+      }
+      step(8, F_{}, T_{}, T_{}, true);
+      step(9, T_{}, T_{}, T_{}, true);
+      step(10, F_{}, T_{}, T_{}, false);
+    } else if constexpr (WV == 3) {   // R 31..40: top only at dl 0, 1
+      step(0, F_{}, T_{}, T_{}, true);
+      step(1, T_{}, T_{}, T_{}, true);
 #pragma unroll 1
-  for (int mt = 2; mt < 4; ++mt) mtile(mt, std::true_type{}, std::true_type{});
+      for (int dl = 2; dl < 10; dl += 2) {
+        step(dl, F_{}, F_{}, T_{}, true);
+        step(dl + 1, T_{}, F_{}, T_{}, dl + 2 < 10);
+      }
+    } else {                          // R 11..30 / 21..30: both
 #pragma unroll 1
-  for (int mt = 4; mt < NMT; ++mt) mtile(mt, std::false_type{}, std::true_type{});
+      for (int dl = 0; dl < 10; dl += 2) {
+        step(dl, F_{}, T_{}, T_{}, true);
+        step(dl + 1, T_{}, T_{}, T_{}, dl + 2 < 10);
+      }
+    }
+  };
+  if constexpr (IVC_ME_PAIR) {
+    mpair(0, std::true_type{}, std::false_type{});
+    mpair(2, std::true_type{}, std::true_type{});
+    mpair(4, std::false_type{}, std::true_type{});
+  } else {
+#pragma unroll 1
+    for (int mt = 0; mt < 2; ++mt) mtile(mt, std::true_type{}, std::false_type{});
+#pragma unroll 1
+    for (int mt = 2; mt < 4; ++mt) mtile(mt, std::true_type{}, std::true_type{});
+#pragma unroll 1
+    for (int mt = 4; mt < NMT; ++mt) mtile(mt, std::false_type{}, std::true_type{});
+  }
   // per block: best -K' over the 16 lanes, then the least raster index among its holders
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -209,9 +302,11 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
         const_cast<uint8_t*>(ref + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint8_t*>(cur + (int64_t)f * HW), 0, exists ? (int)HW : 0, 0x00020000);
+    int tt = tid;
+    asm volatile("" : "+v"(tt));           // (the item offsets: formed per tile, not kept live)
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-      const int i = tid + 256 * k;
+      const int i = tt + 256 * k;
       const int row = i / NPAIR, p = i - row * NPAIR;
       const int y = yb + row;
       const bool ok = i < ITEMS && y >= 0 && y < H;
@@ -235,14 +330,40 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
   Loads L;
   load(tile, L);
   int* red = reinterpret_cast<int*>(lds + RED_OFF);
+  // the merge of the waves' per-block results of a searched tile (threads 0..15, one block
+  // each): run for tile t at the start of tile t + 1, after its first barrier — red[] is next
+  // written by tile t + 1's search, two barriers later — so no barrier of its own and the
+  // other 240 threads stage meanwhile
+  auto merge = [&](uint32_t pf, int pby, int pbx0) {
+    if (tid < 16) {
+      const int blk = tid, bx = pbx0 + (blk & 7), byy = pby + (blk >> 3);
+      int k = red[2 * blk], ri = red[2 * blk + 1];
+#pragma unroll
+      for (int ww = 1; ww < 4; ++ww) {
+        const int ok_ = red[2 * (ww * 16 + blk)], oi = red[2 * (ww * 16 + blk) + 1];
+        if (ok_ > k || (ok_ == k && oi < ri)) {
+          k = ok_;
+          ri = oi;
+        }
+      }
+      if (bx < w && byy < h)
+        mv[((int64_t)pf * h + byy) * w + bx] = ri == INT_MAX ? (int64_t)SR * N + SR : (int64_t)ri;
+    }
+  };
+  uint32_t pf = 0;
+  int pby = 0, pbx0 = 0;
+  bool have_prev = false;
   for (; tile < ntiles; tile += gridDim.x) {
     uint32_t f;
     int by, bx0;
     tile_xy(tile, f, by, bx0);
     __syncthreads();                                   // the previous tile's LDS reads are done
+    if (have_prev) merge(pf, pby, pbx0);
+    int ts = tid;
+    asm volatile("" : "+v"(ts));
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
-      const int i = tid + 256 * k;
+      const int i = ts + 256 * k;
       if (i < ITEMS) {
         const int row = i / NPAIR, p = i - row * NPAIR;
         uint32_t* d = lds + row * PITCH + 2 * p;
@@ -262,7 +383,11 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
       // window energies E[R][u] = B + 128 (-S2') (the header's form), two threads per
       // column u: threads 0..95 the offsets R < 20 from rows 0..26, threads 128..223 the
       // offsets R >= 20 from rows 20..47 (each a prefix over its rows)
-      const int half = tid >> 7, u = tid & 127;
+      const int half = tid >> 7;
+      int u = tid & 127;
+      // (opaque: the per-offset constants derived from u are formed in the tile loop instead of
+      // being hoisted out of it, where they stay live — or spill — through the search)
+      asm volatile("" : "+v"(u));
       if (u < U) {
         const uint32_t* cw = lds + (u & 3) * COPY + (u >> 2);
         const int xb = 8 * bx0 - SR, yb = 8 * by - SR;
@@ -300,22 +425,14 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
     if (wave == 0) me2_search<0>(lds, red, wave, g, l16, bop);
     else if (wave == 3) me2_search<3>(lds, red, wave, g, l16, bop);
     else me2_search<1>(lds, red, wave, g, l16, bop);
-    __syncthreads();
-    if (tid < 16) {
-      const int blk = tid, bx = bx0 + (blk & 7), byy = by + (blk >> 3);
-      int k = red[2 * blk], ri = red[2 * blk + 1];
-#pragma unroll
-      for (int ww = 1; ww < 4; ++ww) {
-        const int ok_ = red[2 * (ww * 16 + blk)], oi = red[2 * (ww * 16 + blk) + 1];
-        if (ok_ > k || (ok_ == k && oi < ri)) {
-          k = ok_;
-          ri = oi;
-        }
-      }
-      if (bx < w && byy < h)
-        mv[((int64_t)f * h + byy) * w + bx] = ri == INT_MAX ? (int64_t)SR * N + SR : (int64_t)ri;
-    }
+    pf = f;
+    pby = by;
+    pbx0 = bx0;
+    have_prev = true;
   }
+  // the last tile's merge (every wave reaches this barrier: the loop bound is workgroup-uniform)
+  __syncthreads();
+  if (have_prev) merge(pf, pby, pbx0);
 }
 
 // A batch of frame pairs on the matrix cores, in launches of under 2^31 tiles (32-bit tile

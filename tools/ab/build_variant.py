@@ -1,5 +1,7 @@
 """Build a libivc variant with extra compiler flags into ab/<name>.so (same sources and flags
-as ivclab_amd/build.py):  python tools/ab/build_variant.py NAME [-DFOO=1 ...]"""
+as ivclab_amd/build.py):  python tools/ab/build_variant.py NAME [-DFOO=1 ...]
+IVC_CSRC=<dir> compiles the sources from another directory (e.g. a copy holding an older
+version of one file)."""
 import os
 import sys
 from concurrent.futures import ThreadPoolExecutor
@@ -14,7 +16,10 @@ os.makedirs(objdir, exist_ok=True)
 os.makedirs(os.path.join(ROOT, "ab"), exist_ok=True)
 flags = [f for f in B.FLAGS if f != "-shared"] + extra
 objs = [os.path.join(objdir, os.path.splitext(f)[0] + ".o") for f in B.SOURCES]
-jobs = [[B.hipcc()] + flags + ["-c", "-o", o, os.path.join(B.CSRC, f)] for f, o in zip(B.SOURCES, objs)]
+csrc = os.environ.get("IVC_CSRC", B.CSRC)
+if csrc != B.CSRC:
+    flags += ["-I" + B.CSRC]
+jobs = [[B.hipcc()] + flags + ["-c", "-o", o, os.path.join(csrc, f)] for f, o in zip(B.SOURCES, objs)]
 with ThreadPoolExecutor(len(jobs)) as ex:
     list(ex.map(lambda c: B._run(c, False), jobs))
 B._run([B.hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o",

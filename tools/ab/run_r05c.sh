@@ -1,0 +1,31 @@
+#!/bin/bash
+# r05c: tiny-call latency breakdown, cfg2 C=3 plane-store A/B + PMC, ME A/B (merge moved, paired
+# M-tile chains) + PMC, then GPU tests + smoke + default bench
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 120 ./tools/ubench/tiny_call > gpurun_out/r05c_tiny_call.log 2>&1 || { tail -20 gpurun_out/r05c_tiny_call.log; exit 1; }
+cat gpurun_out/r05c_tiny_call.log
+timeout -k 10 600 python tools/ab/ab_cfg2.py ab/c3base.so ab/c3pst.so --rounds 5 > gpurun_out/r05c_ab_cfg2.log 2>&1 || { tail -20 gpurun_out/r05c_ab_cfg2.log; exit 1; }
+cat gpurun_out/r05c_ab_cfg2.log
+timeout -k 10 600 python tools/ab/ab_me.py ab/mebase.so ab/memerge.so ab/mepair0.so ab/mepair.so --rounds 4 --oracle > gpurun_out/r05c_ab_me.log 2>&1 || { tail -20 gpurun_out/r05c_ab_me.log; exit 1; }
+cat gpurun_out/r05c_ab_me.log
+for v in c3base c3pst; do
+  CHILD="tools/cfg2_pmc_child.py ab/$v.so" PMC_GROUPS=tools/pmc_groups_luma.txt OUTDIR=r05c_pmc_$v timeout -k 10 600 bash tools/gpu_pmc_child.sh > gpurun_out/r05c_pmc_$v.log 2>&1 || { tail -20 gpurun_out/r05c_pmc_$v.log; exit 1; }
+done
+ME_NO_F64=1 CHILD="tools/me_pmc_child.py" PMC_GROUPS=tools/pmc_groups_me.txt OUTDIR=r05c_pmc_me timeout -k 10 600 bash tools/gpu_pmc_child.sh > gpurun_out/r05c_pmc_me.log 2>&1 || { tail -20 gpurun_out/r05c_pmc_me.log; exit 1; }
+echo pmc ok
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r05c_pytest.log 2>&1 || { tail -40 gpurun_out/r05c_pytest.log; exit 1; }
+tail -3 gpurun_out/r05c_pytest.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05c_smoke.log 2>&1 || { tail -20 gpurun_out/r05c_smoke.log; exit 1; }
+echo smoke ok
+timeout -k 10 600 python bench.py > gpurun_out/r05c_bench.json 2> gpurun_out/r05c_bench.err || { tail -20 gpurun_out/r05c_bench.err; exit 1; }
+python -c "
+import json; p=json.load(open('gpurun_out/r05c_bench.json'))
+print('headline', p['value'], p['roofline']['frac'])
+for k in ['image2symbols','zerorun','decode']: print(k, p[k].get('ms'))
+print('inter', p['inter']['ms_per_step'], p['inter']['roofline']['kernel_ms'])
+print('cfg2', p['cfg2']['one_frame']['ms_per_launch'], p['cfg2']['batch_64']['ms_per_launch'])
+print('small', p['class_api']['small_call'])
+"

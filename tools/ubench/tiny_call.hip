@@ -1,0 +1,110 @@
+// Latency breakdown of a tiny host-buffer call (one 8x8 block, the reference's per-block loops,
+// exercises/ch3/E3-1_claude.py:47-60): what a launch, the completion wait and the mapped-memory
+// access each cost, against the whole C-ABI call (ivc_dct8x8 on a u8 block).
+//   hipcc --offload-arch=gfx950 -O2 tools/ubench/tiny_call.hip -Iinclude -Livclab_amd/_lib -livc \
+//         -Wl,-rpath,$PWD/ivclab_amd/_lib -o /tmp/tiny_call && /tmp/tiny_call
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <string.h>
+#include <algorithm>
+#include <chrono>
+#include <vector>
+#include "ivc.h"
+
+__global__ void empty_k() {}
+__global__ void flag_k(unsigned* flag, unsigned seq) {
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+// 64 lanes read 8 bytes each of a mapped input and write 8 doubles each to a mapped output
+__global__ void io_k(const uint8_t* in, double* out, unsigned* flag, unsigned seq) {
+  const int t = threadIdx.x;
+  double v = (double)in[t];
+  out[t] = v * 0.5;
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+template <typename F>
+static void run(const char* name, F&& f, int n = 3000) {
+  std::vector<double> t(n);
+  for (int i = 0; i < 200; ++i) f(i);
+  for (int i = 0; i < n; ++i) {
+    const double a = now_us();
+    f(i);
+    t[i] = now_us() - a;
+  }
+  std::sort(t.begin(), t.end());
+  double s = 0;
+  for (double x : t) s += x;
+  printf("%-58s median %7.2f us  p10 %7.2f  p90 %7.2f  mean %7.2f\n", name, t[n / 2], t[n / 10],
+         t[9 * n / 10], s / n);
+}
+
+int main() {
+  hipStream_t s;
+  (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  hipEvent_t ev;
+  (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  unsigned* flag;
+  (void)hipHostMalloc((void**)&flag, 4096, hipHostMallocDefault);
+  uint8_t* min;
+  double* mout;
+  (void)hipHostMalloc((void**)&min, 4096, hipHostMallocDefault);
+  (void)hipHostMalloc((void**)&mout, 4096, hipHostMallocDefault);
+  *flag = 0;
+  run("hipStreamSynchronize, idle stream", [&](int) { (void)hipStreamSynchronize(s); });
+  run("launch empty kernel (host API only)", [&](int) { empty_k<<<1, 64, 0, s>>>(); });
+  (void)hipStreamSynchronize(s);
+  run("launch empty kernel + hipStreamSynchronize", [&](int) {
+    empty_k<<<1, 64, 0, s>>>();
+    (void)hipStreamSynchronize(s);
+  });
+  run("launch empty kernel + event record + hipEventSynchronize", [&](int) {
+    empty_k<<<1, 64, 0, s>>>();
+    (void)hipEventRecord(ev, s);
+    (void)hipEventSynchronize(ev);
+  });
+  run("launch empty kernel + hipStreamQuery spin", [&](int) {
+    empty_k<<<1, 64, 0, s>>>();
+    while (hipStreamQuery(s) == hipErrorNotReady) {}
+  });
+  unsigned seq = 1;
+  run("launch flag kernel + host spin on mapped flag", [&](int) {
+    const unsigned q = ++seq;
+    flag_k<<<1, 64, 0, s>>>(flag, q);
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+  });
+  (void)hipStreamSynchronize(s);
+  run("launch io kernel (64 B in, 512 B out, mapped) + spin", [&](int) {
+    const unsigned q = ++seq;
+    io_k<<<1, 64, 0, s>>>(min, mout, flag, q);
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+  });
+  (void)hipStreamSynchronize(s);
+  run("launch io kernel + hipStreamSynchronize", [&](int) {
+    const unsigned q = ++seq;
+    io_k<<<1, 64, 0, s>>>(min, mout, flag, q);
+    (void)hipStreamSynchronize(s);
+  });
+  uint8_t blk[64];
+  double out[64];
+  for (int i = 0; i < 64; ++i) blk[i] = (uint8_t)(i * 7);
+  run("ivc_dct8x8 u8 (8,8) -> f64 host call (the C-ABI tiny path)", [&](int) {
+    if (ivc_dct8x8(blk, IVC_U8, 1, out, IVC_F64, 0, IVC_NORM_ORTHO) != 0) printf("err %s\n", ivc_last_error());
+  });
+  double q3[192], tb[192];
+  int32_t qo[192];
+  for (int i = 0; i < 192; ++i) { q3[i] = i * 3.7 - 300; tb[i] = 16 + i % 40; }
+  run("ivc_quantize f64 (3,8,8) host call", [&](int) {
+    if (ivc_quantize(q3, IVC_F64, 1, 3, tb, IVC_F64, qo) != 0) printf("err %s\n", ivc_last_error());
+  });
+  return 0;
+}
