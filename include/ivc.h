@@ -105,7 +105,7 @@ int ivc_set_store_pace(double total_gbps);
 double ivc_store_pace(void);
 double ivc_store_pace_late(void);
 /* Measurement statistics of the current device's paced launches since the last reset
- * (encoder 0 = image source, 1 = inter residual, 2 = luma-only image, 3 = 3-channel image), folding every completed launch first:
+ * (encoder 0 = image source, 1 = inter residual, 2 = luma-only image), folding every completed launch first:
  * out[0] launches measured, [1] launches over the late threshold, [2] mean and [3] maximum
  * late fraction, [4] current rate (GB/s), [5] last late fraction, [6] mean achieved GB/s of
  * the measured launches (bytes / event time), [7] measurements still in flight, [8] launches

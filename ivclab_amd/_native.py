@@ -7,8 +7,11 @@ built in-tree by `python -m ivclab_amd.build` (or __graft_entry__.build()).
 from __future__ import annotations
 
 import ctypes as _ct
+from ctypes import addressof as _addressof, c_char as _c_char
+import math
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -184,7 +187,14 @@ def check(status: int, what: str = "ivc") -> None:
 
 
 def ptr(a: np.ndarray) -> int:
-    return a.ctypes.data
+    # Address of the first element.  a.ctypes.data builds a ctypes object per call (~1 us on the
+    # GPU box's host, as long as the DCT kernel's host side of a per-block loop call): the
+    # buffer address of a writable C-contiguous array is 3x cheaper; anything else (read-only,
+    # strided, empty) takes the array interface.
+    try:
+        return _addressof(_c_char.from_buffer(a))
+    except (TypeError, ValueError, BufferError):
+        return a.__array_interface__["data"][0]
 
 
 def pace_stats(encoder: int = 0):
@@ -220,10 +230,9 @@ def empty(shape, dtype) -> np.ndarray:
     array is large (>= 1 MiB): the device writes it with one DMA and no staging copy.  The
     block returns to the pool when the array (and every view of it) is garbage collected.
     Falls back to np.empty when no device library is usable or pinning fails."""
-    import weakref
     dtype = np.dtype(dtype)
     shape = tuple(int(d) for d in (shape if np.iterable(shape) else (shape,)))
-    count = int(np.prod(shape, dtype=np.int64))
+    count = math.prod(shape)                 # (np.prod costs ~5 us per call: per-block loops)
     nbytes = count * dtype.itemsize
     if nbytes < _PINNED_MIN:
         return np.empty(shape, dtype)

@@ -11,6 +11,7 @@
 #include <list>
 #include <map>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -169,6 +170,7 @@ struct DevCtx {
   int aux_state = 0;                        // 0 untried, 1 ready, -1 unavailable
   void* tiny = nullptr;                     // page-locked, device-mapped block for tiny calls
   int tiny_state = 0;                       // 0 untried, 1 ready, -1 unavailable
+  uint32_t tiny_seq = 0;                    // last completion value written behind a tiny call
   void* slot[kSlots] = {};
   size_t cap[kSlots] = {};
   void* pin[kPinSlots] = {};
@@ -191,9 +193,12 @@ bool aux_ready(DevCtx* c) {
 }
 
 constexpr size_t kTinyMax = 64u << 10;      // bytes of input and of output for a tiny call
+// after the input and output blocks: the completion word a tiny call's stream writes
+constexpr size_t kTinyFlag = 2 * kTinyMax;
 bool tiny_ready(DevCtx* c) {
   if (c->tiny_state == 0) {
-    c->tiny_state = hipHostMalloc(&c->tiny, 2 * kTinyMax, hipHostMallocDefault) == hipSuccess ? 1 : -1;
+    c->tiny_state = hipHostMalloc(&c->tiny, 2 * kTinyMax + 256, hipHostMallocDefault) == hipSuccess ? 1 : -1;
+    if (c->tiny_state == 1) *reinterpret_cast<volatile uint32_t*>((char*)c->tiny + kTinyFlag) = 0;
     (void)hipGetLastError();
   }
   return c->tiny_state == 1;
@@ -370,15 +375,40 @@ struct Staging {
   // device addresses directly, the kernel reads it and writes its output there over the bus
   // (no DMA transfers to set up), then one sync and a copy out: one launch per call.
   // Returns false, nothing done, when the sizes do not qualify.
+  //   Completion: the stream writes a sequence number into a page-locked word behind the kernel
+  // (hipStreamWriteValue32: a command-processor write, no second kernel) and the host spins on
+  // it — a blocking hipStreamSynchronize costs ~5 us more per call (tools/ubench/tiny_call.hip,
+  // profiles/r05c_tiny_call.log).  The spin gives up after 50 ms and synchronises, which also
+  // reports a failed kernel; a stream that cannot write values synchronises at once.
   template <typename L>
   bool tiny(const void* src, size_t IB, void* dst, size_t OB, const char* what, L&& launch) {
     if (status || IB > kTinyMax || OB > kTinyMax || !tiny_ready(ctx)) return false;
     char* ti = (char*)ctx->tiny;
     char* to = ti + kTinyMax;
+    uint32_t* flag = reinterpret_cast<uint32_t*>(ti + kTinyFlag);
     if (IB) memcpy(ti, src, IB);
     if (launched(launch(ti, to, ctx->stream), what)) return true;
-    hipError_t e = hipStreamSynchronize(ctx->stream);
-    if (e != hipSuccess) { status = fail_hip(e, "hipStreamSynchronize"); return true; }
+    const uint32_t seq = ++ctx->tiny_seq;
+    bool done = false;
+    if (hipStreamWriteValue32(ctx->stream, flag, seq, 0) == hipSuccess) {
+      const auto t0 = std::chrono::steady_clock::now();
+      for (uint32_t i = 1;; ++i) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) {
+          done = true;
+          break;
+        }
+        __builtin_ia32_pause();
+        if ((i & 1023u) == 0 &&
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+          break;
+      }
+    } else {
+      (void)hipGetLastError();
+    }
+    if (!done) {
+      hipError_t e = hipStreamSynchronize(ctx->stream);
+      if (e != hipSuccess) { status = fail_hip(e, "hipStreamSynchronize"); return true; }
+    }
     if (OB) memcpy(dst, to, OB);
     return true;
   }
@@ -554,8 +584,8 @@ double ivc_store_pace(void) { return store_pace_gbps(); }
 double ivc_store_pace_late(void) { return store_pace_late_fraction(); }
 
 int ivc_store_pace_stats(int encoder, double* out, int n) {
-  if (encoder < 0 || encoder > 3 || n < 0 || (n > 0 && !out))
-    return fail(IVC_E_ARG, "ivc_store_pace_stats: encoder must be 0..3, out must hold n values");
+  if (encoder < 0 || encoder > 2 || n < 0 || (n > 0 && !out))
+    return fail(IVC_E_ARG, "ivc_store_pace_stats: encoder must be 0, 1 or 2, out must hold n values");
   return store_pace_stats(encoder, out, n);
 }
 
@@ -565,8 +595,8 @@ int ivc_store_pace_reset_stats(void) {
 }
 
 int ivc_store_pace_trace(int encoder, double* out, int max_records) {
-  if (encoder < 0 || encoder > 3 || max_records < 0 || (max_records > 0 && !out))
-    return fail(IVC_E_ARG, "ivc_store_pace_trace: encoder must be 0..3, out must hold "
+  if (encoder < 0 || encoder > 2 || max_records < 0 || (max_records > 0 && !out))
+    return fail(IVC_E_ARG, "ivc_store_pace_trace: encoder must be 0, 1 or 2, out must hold "
                            "7 * max_records values");
   return store_pace_trace(encoder, out, max_records);
 }

@@ -360,6 +360,8 @@ struct FusedArgs {
   uint32_t nframes;      // number of output frames F
   int H, W, h, w, tpr;   // tpr = tiles (of 8 blocks) per block row
   int sr;
+  int split3;            // C = 3 coefficients: one wave per (group, plane) instead of per group
+                         // (small launches: three times the waves, each a third of the work)
   int dup12;             // table planes 1 and 2 identical (always true for PatchQuant tables);
                          // C = 1 kernels take it as the template flag DUP
   // zero-run symbol modes (OUTM = OUT_COUNT / OUT_SYMBOLS): per-group symbol counts, their
@@ -425,6 +427,12 @@ struct FusedArgs {
 #endif
 #ifndef IVC_C3_PLANE_STORE
 #define IVC_C3_PLANE_STORE 1   // C = 3 coefficients: each plane stored as soon as it is quantised
+#endif
+#ifndef IVC_C3_SPLIT
+#define IVC_C3_SPLIT 1         // C = 3 coefficients, small launches: one wave per (group, plane)
+#endif
+#ifndef IVC_C3_WAVES
+#define IVC_C3_WAVES 1         // C = 3 coefficients: min waves per SIMD the registers must allow
 #endif
 
 constexpr int XS_PITCH = 72;   // T elements per block in the transpose image
@@ -714,9 +722,10 @@ template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SR
 __device__ __forceinline__ void encode_group(const FusedArgs& a, const RowReg<TI, C, SRC>& v,
                                              T* xs, int32_t* os, const double* srq, const D* sq,
                                              int b, int r, uint32_t zp0, uint32_t zp1,
-                                             PlaneDone plane_done = NoPlaneDone{}) {
+                                             PlaneDone plane_done = NoPlaneDone{}, int conly = -1) {
 #pragma unroll
   for (int c = 0; c < C; ++c) {
+    if (conly >= 0 && c != conly) continue;       // (split3: this wave's one plane)
     // ---- row pass (axis -1): lane owns row r of block b ------------------------------------
     T x[8];
     if constexpr (FAST) {
@@ -1281,7 +1290,9 @@ __device__ __forceinline__ void coef_hist(const FusedArgs& a, const int32_t* os,
 
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
           int NG, bool DUP, int OUTM = OUT_COEFS>
-__global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && C == 1 && DUP) ? 6 : 1) void fused_encode_kernel(FusedArgs a, QTab t) {
+__global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && C == 1 && DUP) ? 6
+                                  : (C == 3 && OUTM == OUT_COEFS ? IVC_C3_WAVES : 1))
+void fused_encode_kernel(FusedArgs a, QTab t) {
   static_assert(OUTM == OUT_COEFS || OUTM == OUT_LUMA || OUTM == OUT_COEFH || (ZZ && SRC == SRC_IMAGE),
                 "symbols need zig-zag order");
   static_assert(OUTM != OUT_LUMA || C == 1, "the luma-only output is for C = 1 images");
@@ -1368,7 +1379,24 @@ __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && 
   bool have_prev = false;
 
   constexpr int PF = (SRC == SRC_IMAGE && TileRaw<TI, C, NG>::NW <= 8) ? IVC_PREFETCH : 1;
-  if constexpr (PF > 1) {
+  if (PST && a.split3) {
+    // one wave per (group, plane): virtual unit vt = 3 lt + c; the group's rows are loaded
+    // whole (the wave uses one channel of them) and its plane stored as soon as it is quantised
+    if constexpr (PST) {
+      const uint32_t nvt = 3u * nlt;
+      for (uint32_t vt = lt; vt < nvt; vt += nwaves) {
+        const uint32_t t3 = vt / 3u;
+        const int c = (int)(vt - 3u * t3);
+        TileRaw<TI, C, NG> raw;
+        load_tile<TI, C, NG>(a, t3, true, lane, raw);
+        RowReg<TI, C, SRC> v;
+        group_row<TI, C, NG>(raw, 0, lane, v);
+        encode_group<TI, T, D, C, FAST, ZZ, SRC, CHECKMAG, DUP, false, PST>(
+            a, v, xs, os, srq, sq, b, r, zp0, zp1,
+            [&](int cc) { store_plane<NG>(a, os, lane, t3, 0, cc, !IVC_SKIP(a, 16)); }, c);
+      }
+    }
+  } else if constexpr (PF > 1) {
     // Software pipeline per wave in rounds of PF load tiles (nwaves apart).  At the start of
     // a round the wave issues the loads of the whole next round at once, so the chip's read
     // stream arrives in bursts between long runs of stores instead of an even 1:12 mix with
@@ -1619,7 +1647,7 @@ struct PaceState {
   int64_t gen = 0;                // bumped by ivc_set_store_pace: older launches are not folded
 };
 // per device and per encoder (0: image source, 1: inter residual source, 2: luma-only image)
-static PaceState g_pace[64][4];
+static PaceState g_pace[64][3];
 
 static double pace_start_rate() {
   if (g_pace_start < 0) {
@@ -1904,15 +1932,26 @@ static void launch_fused_one(const FusedArgs& a_in, const QTab& t, hipStream_t s
   const double out_bytes = OUTM == OUT_LUMA ? 256.0 : 768.0;
   const double gbytes = 8.0 * (SRC == SRC_INTER ? 64.0 * 2 + 8.0 + out_bytes
                                                 : 64.0 * C * sizeof(TI) + out_bytes);
-  // pacing state per encoder: image source, inter residual, luma-only image, 3-channel image
-  // (each adapts its own rate: a 3-channel launch runs at a different pace than a luma one)
-  const int kind = OUTM == OUT_LUMA ? 2 : (C == 3 && SRC == SRC_IMAGE ? 3 : SRC);
+  // pacing state per encoder: image source, inter residual, luma-only image
+  const int kind = OUTM == OUT_LUMA ? 2 : SRC;
+  // unpaced: the luma-only variant (its PMC, profiles/r04g_pmc_luma.json, shows it issue-bound,
+  // not store-order-bound, and faster without the schedule) and the 3-channel image encoder
+  // (cfg2, 64 x 1080p RGB: 0.429 ms unpaced against 0.445-0.493 ms paced at any start rate,
+  // profiles/r05d_ab_cfg2.log — it is issue/latency-bound, 3 transforms per 8-block group)
+  constexpr bool unpaced = OUTM == OUT_LUMA || (C == 3 && SRC == SRC_IMAGE);
   auto go = [&](auto k) {
+    // 3-channel coefficients, few groups (fewer than 2 per resident wave: one frame of cfg2):
+    // one wave per (group, plane)
+    if (C == 3 && OUTM == OUT_COEFS && SRC == SRC_IMAGE && IVC_C3_PLANE_STORE && IVC_C3_SPLIT &&
+        nlt < 8 * (int64_t)resident_grid(k, (int64_t)1 << 40)) {
+      a.split3 = 1;
+      const unsigned g3 = resident_grid(k, (3 * nlt + 3) / 4);
+      k<<<g3, 256, 0, s>>>(a, t);
+      return;
+    }
     const unsigned g = grid(k);
     const int64_t nw = 4 * (int64_t)g;
-    // the luma-only variant runs unpaced: its PMC (profiles/r04g_pmc_luma.json) shows it
-    // issue-bound, not store-order-bound, and faster without the schedule
-    const int slot = OUTM == OUT_LUMA ? -1 : setup_pacing(a, kind, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
+    const int slot = unpaced ? -1 : setup_pacing(a, kind, nw, (nlt + nw - 1) / nw * NG, gbytes, s);
     k<<<g, 256, 0, s>>>(a, t);
     finish_pacing(kind, slot, s);
   };
@@ -1968,6 +2007,7 @@ static FusedArgs make_fused_args(const void* img, const int64_t* mv, int32_t* ou
   a.pace_t0 = nullptr;
   a.pace_d = 0;
   a.pace_early = 0;
+  a.split3 = 0;
   a.dup12 = 1;
   for (int i = 0; i < 64; ++i)
     if (t.q[64 + i] != t.q[128 + i]) a.dup12 = 0;

@@ -49,7 +49,7 @@ constexpr int MASK_C = -(1 << 22);               // C of a (block, window) pair 
 typedef int mf_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned int mf_u32x2 __attribute__((ext_vector_type(2)));
 #ifndef IVC_ME_PAIR
-#define IVC_ME_PAIR 1
+#define IVC_ME_PAIR 0
 #endif
 
 // ---- two block rows per tile --------------------------------------------------

@@ -116,6 +116,50 @@ def test_tiny_calls_zero_copy():
         assert_bits(z, O.zigzag_scan(blk.astype(np.int32)), "zigzag_scan")
 
 
+def test_tiny_call_fast_paths_match_general_path():
+    """The per-block fast paths of DCT.transform / PatchQuant.quantize / dequantize (small
+    arrays straight to the C-ABI, cached table) give the general path's bits and the oracle's
+    on what the reference's per-block loops pass (exercises/ch3/E3-1_claude.py:47-60: one
+    channel of a patch view — non-contiguous float32 — then the (3, 8, 8) stack), read-only
+    and byte-swapped inputs, C = 1 stacks that broadcast, and a table edited in place or a
+    scale replaced between calls (the cache must notice)."""
+    rng = np.random.default_rng(77)
+    img = (rng.integers(0, 256, (64, 48, 3)).astype(np.float32) - 128.0)
+    patches = Patcher().patch(img)                       # [h, w, c, 8, 8] view
+    pq = PatchQuant()
+    for h, w in ((0, 0), (3, 2), (7, 5)):
+        blk3 = patches[h, w]                             # (3, 8, 8) view
+        dct3 = np.zeros_like(blk3, dtype=np.float32)
+        for c in range(3):
+            dct3[c] = DCT.transform(blk3[c])             # non-contiguous (8, 8) float32
+            assert_bits(DCT.transform(blk3[c]), O.dct_transform(np.ascontiguousarray(blk3[c])), "view")
+        assert_bits(pq.quantize(dct3), O.quantize(dct3, 1.0), "E3-1 quantize")
+    x = rng.normal(0, 50, (8, 8))
+    ro = x.copy()
+    ro.flags.writeable = False
+    assert_bits(DCT.transform(ro), O.dct_transform(x), "read-only")
+    sw = x.astype(">f8")                                  # not a kernel dtype: the general path
+    assert_bits(DCT.transform(sw), O.dct_transform(x), "byte-swapped")
+    one = rng.normal(0, 30, (1, 8, 8))
+    assert_bits(pq.quantize(one), O.quantize(one, 1.0), "C = 1 stack")
+    assert pq.quantize(one).shape == (1, 1, 3, 8, 8)
+    many = rng.normal(0, 30, (2, 3, 1, 8, 8))
+    assert_bits(pq.quantize(many), O.quantize(many, 1.0), "C = 1 batch")
+    stk = rng.normal(0, 40, (3, 8, 8))
+    pq2 = PatchQuant(0.5)
+    before = pq2.quantize(stk)
+    pq2.luminance[0, 0] = 3.0                             # edited in place
+    want = np.round(stk / pq2.get_quantization_table()[None, None]).astype(np.int32)
+    assert_bits(pq2.quantize(stk), want, "edited luminance")
+    assert not np.array_equal(before, want)
+    pq2.quantization_scale = np.float64(0.25)             # a NumPy scalar: float64 table
+    want = np.round(stk / pq2.get_quantization_table()[None, None]).astype(np.int32)
+    assert_bits(pq2.quantize(stk), want, "new scale")
+    q = pq2.quantize(stk)
+    assert_bits(pq2.dequantize(q), (q * pq2.get_quantization_table()[None, None]).astype(np.int32),
+                "dequantize")
+
+
 def test_dct_golden(golden):
     d = golden("dct")
     assert_bits(DCT.transform(d["x_u8"]), d["dct_u8"], "dct u8")

@@ -89,6 +89,20 @@ int main() {
     while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
   });
   (void)hipStreamSynchronize(s);
+  run("launch io kernel + hipStreamWriteValue32 + spin", [&](int) {
+    const unsigned q = ++seq;
+    io_k<<<1, 64, 0, s>>>(min, mout, flag + 16, q);
+    (void)hipStreamWriteValue32(s, flag, q, 0);
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+  });
+  (void)hipStreamSynchronize(s);
+  run("launch empty kernel + hipStreamWriteValue32 + spin", [&](int) {
+    const unsigned q = ++seq;
+    empty_k<<<1, 64, 0, s>>>();
+    (void)hipStreamWriteValue32(s, flag, q, 0);
+    while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+  });
+  (void)hipStreamSynchronize(s);
   run("launch io kernel + hipStreamSynchronize", [&](int) {
     const unsigned q = ++seq;
     io_k<<<1, 64, 0, s>>>(min, mout, flag, q);
