@@ -193,6 +193,13 @@ bool aux_ready(DevCtx* c) {
 }
 
 constexpr size_t kTinyMax = 64u << 10;      // bytes of input and of output for a tiny call
+// the completion word of a tiny call: written after everything before it on the stream
+__global__ void tiny_signal_kernel(uint32_t* flag, uint32_t seq) {
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
 // after the input and output blocks: the completion word a tiny call's stream writes
 constexpr size_t kTinyFlag = 2 * kTinyMax;
 bool tiny_ready(DevCtx* c) {
@@ -375,11 +382,11 @@ struct Staging {
   // device addresses directly, the kernel reads it and writes its output there over the bus
   // (no DMA transfers to set up), then one sync and a copy out: one launch per call.
   // Returns false, nothing done, when the sizes do not qualify.
-  //   Completion: the stream writes a sequence number into a page-locked word behind the kernel
-  // (hipStreamWriteValue32: a command-processor write, no second kernel) and the host spins on
-  // it — a blocking hipStreamSynchronize costs ~5 us more per call (tools/ubench/tiny_call.hip,
-  // profiles/r05c_tiny_call.log).  The spin gives up after 50 ms and synchronises, which also
-  // reports a failed kernel; a stream that cannot write values synchronises at once.
+  //   Completion: a one-wave kernel behind the op writes a sequence number into a page-locked
+  // word (system-scope release) and the host spins on it.  Per call (tools/ubench/tiny_call.hip,
+  // profiles/r05e_tiny_call.log): a blocking hipStreamSynchronize costs ~5 us more, and
+  // hipStreamWriteValue32 (a command-processor write) ~2.5 us more than the kernel.  The spin
+  // gives up after 50 ms and synchronises, which also reports a failed kernel.
   template <typename L>
   bool tiny(const void* src, size_t IB, void* dst, size_t OB, const char* what, L&& launch) {
     if (status || IB > kTinyMax || OB > kTinyMax || !tiny_ready(ctx)) return false;
@@ -390,7 +397,8 @@ struct Staging {
     if (launched(launch(ti, to, ctx->stream), what)) return true;
     const uint32_t seq = ++ctx->tiny_seq;
     bool done = false;
-    if (hipStreamWriteValue32(ctx->stream, flag, seq, 0) == hipSuccess) {
+    tiny_signal_kernel<<<1, 64, 0, ctx->stream>>>(flag, seq);
+    if (hipGetLastError() == hipSuccess) {
       const auto t0 = std::chrono::steady_clock::now();
       for (uint32_t i = 1;; ++i) {
         if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) {

@@ -1304,14 +1304,20 @@ void fused_encode_kernel(FusedArgs a, QTab t) {
   typedef WaveLds<T, C, DUP, PST> L;
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
   __shared__ double srq[FAST ? 192 : 1];
-  __shared__ D sq[192];
+  // the table itself: staged for the division path (!FAST); the FAST path divides only in its
+  // rare exact fallback and reads the kernel argument there (1.5 KB less LDS: the C = 3
+  // encoder fits 8 workgroups per CU)
+  __shared__ D sq_lds[FAST ? 1 : 192];
+  const D* sq;
+  if constexpr (FAST) sq = t.q;
+  else sq = sq_lds;
   __shared__ uint32_t zh[OUTM == OUT_SYMH || OUTM == OUT_COEFH ? ZH_LDS : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   const int b = lane >> 3, r = lane & 7;
   if (a.zr_gate && *a.zr_gate == 0) return;           // (the emitter's fallback, not needed)
   for (int i = tid; i < 192; i += 256) {
-    sq[i] = (D)t.q[i];
+    if constexpr (!FAST) sq_lds[i] = (D)t.q[i];
     // s_i * s_k * RN(1/q): the DCT's power-of-two output scales folded into the reciprocal
     // (1.0 / q is IEEE-correctly rounded here as on the host)
     if constexpr (FAST) srq[i] = (dct2_scale((i >> 3) & 7) * dct2_scale(i & 7)) * (1.0 / t.q[i]);
@@ -1378,7 +1384,9 @@ void fused_encode_kernel(FusedArgs a, QTab t) {
   int pg = 0;
   bool have_prev = false;
 
-  constexpr int PF = (SRC == SRC_IMAGE && TileRaw<TI, C, NG>::NW <= 8) ? IVC_PREFETCH : 1;
+  // (3-channel images: one tile ahead — the two-tile rounds measured slower there, 0.4266 vs
+  // 0.4198 ms for 64 x 1080p RGB and 14.9 vs 8.7 us for one frame, profiles/r05e_ab_cfg2.log)
+  constexpr int PF = (SRC == SRC_IMAGE && TileRaw<TI, C, NG>::NW <= 8) ? (C == 3 ? 1 : IVC_PREFETCH) : 1;
   if (PST && a.split3) {
     // one wave per (group, plane): virtual unit vt = 3 lt + c; the group's rows are loaded
     // whole (the wave uses one channel of them) and its plane stored as soon as it is quantised

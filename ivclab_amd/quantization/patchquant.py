@@ -43,6 +43,8 @@ def _as_blocks(x: np.ndarray, table: np.ndarray):
 
 
 def _kernel_input(x: np.ndarray) -> np.ndarray:
+    if not x.dtype.isnative:
+        x = x.astype(x.dtype.newbyteorder("="))       # same values in the host byte order
     if x.dtype == np.bool_:
         return x.view(np.uint8)
     if x.dtype == np.float16:

@@ -59,6 +59,8 @@ def dct2d(a, norm="ortho", inverse=False) -> np.ndarray:
     if x.shape[-2:] != (8, 8):
         raise NotImplementedError(
             f"ivclab_amd: DCT is implemented for 8x8 blocks (the codec block size); got {x.shape[-2:]}")
+    if not x.dtype.isnative:
+        x = x.astype(x.dtype.newbyteorder("="))   # same values in the host byte order
     if x.dtype == np.float16:
         x = x.astype(np.float32)          # scipy's _asfarray does the same
     elif x.dtype == np.bool_:
