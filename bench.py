@@ -20,7 +20,7 @@ Also reported from the same run (each with its own timing; none of them is `valu
   exchange                 global Huffman-table input: alphabet bounds (all-reduce) and the
                            symbol histogram (all-gather), as IntraCodec trains it
   inter                    configs[3]: 1080p x 300, +-16 full-search ME + MC + residual
-                           DCT+quant; `roofline` of the motion search (dot4-VALU bound)
+                           DCT+quant; issue roofline of the matrix-core motion search
   inter_f64                the ME VideoCodec really runs: NumPy-semantics float64 SSD
                            (pairwise order) on non-integer 1080p luma, +-16; FP64-VALU roofline
   class_api                host buffers through the drop-in classes (DCT.transform ->
@@ -63,6 +63,11 @@ HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
 #   v_dot4_u32_u8 issues at half rate (tools/ubench/valu_rates.hip): 39.3 T lane-instr/s
 #   FP64 add/mul (no FMA: NumPy rounds every product): half the FP32 vector rate, 39.3 T op/s
 DOT4_PEAK_T = 256 * 4 * 64 * 2.4e9 / 4 / 1e12
+# issue roofline of the +-16 matrix-core search (leg_inter): per-tile instruction counts from
+# its PMC (profiles/r05_pmc_me.json), issue costs and capacity as in leg_inter
+ME_VALU_PER_TILE, ME_MFMA_PER_TILE = 2843, 246
+VALU_ISSUE_CYC, MFMA_ISSUE_CYC = 2.49, 8
+ISSUE_PEAK_T = 256 * 4 * 2.1e9 / 1e12
 # dense i8 MFMA: twice the bf16 rate (MI355X_MICROARCH.md: ~2.5 PF bf16 dense)
 MFMA_I8_PEAK_T = 5000.0
 F64_PEAK_T = 78.6 / 2
@@ -750,40 +755,50 @@ def leg_inter(args, dist, rank, world, dev, table, result, verify):
         D.inter_encode(seq, sr, table, mv, q, zigzag=args.zigzag)
 
     iwall, ims = timed(dist, istep, args.inter_steps, 1)
-    # the motion search alone (the matrix-core search, or the S2 pre-pass + dot4 search kernels
-    # chunked as inside inter_encode when IVC_ME_MFMA=0), timed with events on its stream
-    from ivclab_amd import _native as N
-    mfma = bool(N.lib().ivc_me_mfma_enabled())
+    # the motion search alone (the matrix-core search), timed with events on its stream
     mv2 = torch.empty_like(mv)
     _, me_ms = timed(None, lambda: D.motion_estimate(seq[:-1], seq[1:], sr, mv2, exact_u8=True),
                      args.inter_steps, 1)
     ipx = (Fi - 1) * Hi * Wi
     cand = valid_candidates(Hi, Wi, sr) * (Fi - 1)
-    dot4 = cand * 16                        # 64 px of c*r per candidate = 16 v_dot4 lane-ops
     macs = cand * 64                        # useful multiply-adds (window x block) per search
+    # issue roofline of me_mfma16x2_kernel (the counters show its VALU issue, not the matrix
+    # cores, binding: profiles/r05_pmc_me.json): per tile of 2 x 8 blocks the kernel issues
+    # ME_VALU_PER_TILE vector and ME_MFMA_PER_TILE v_mfma_i32_16x16x64_i8 instructions (static
+    # per tile: no data-dependent branches); a wave64 integer VALU instruction costs its SIMD
+    # 2.49 issue cycles at full occupancy (tools/ubench/valu_rates.hip), an MFMA holds the SIMD's
+    # vector issue for 8 (MI355X guide, cycle constants); capacity = 1024 SIMDs x 2.1 GHz
+    tiles = (Fi - 1) * ((Hi // 8 + 1) // 2) * ((Wi // 8 + 7) // 8)
+    issue = tiles * (ME_VALU_PER_TILE * VALU_ISSUE_CYC + ME_MFMA_PER_TILE * MFMA_ISSUE_CYC)
+    live_ops = tiles * ME_MFMA_PER_TILE * 16 * 16 * 64 * 2     # every MFMA output, live or masked
+    dot4 = cand * 16
     result["inter"] = {
         "metric": "Mpixels/s: 1080p +-16 full-search ME + MC + residual DCT+quant",
         "value": round(world * ipx * args.inter_steps / iwall / 1e6, 1), "unit": "Mpixels/s",
         "ms_per_step": round(iwall / args.inter_steps * 1e3, 3),
         "config": {"workload": f"cfg4: {Fi} frames 1920x1080 u8 luma per GPU, sr={sr}, "
                                "ME against the previous source frame (open loop)"},
-        "roofline": {"bound": "latency (LDS / barriers; issue ~40%)" if mfma else "valu (v_dot4_u32_u8)",
-                     "kernel": "me_mfma16x2_kernel" if mfma else "me_s2_kernel<true> + me_tile16_kernel",
+        "roofline": {"bound": "issue (VALU + MFMA issue slots; PMC)",
+                     "kernel": "me_mfma16x2_kernel",
                      "kernel_ms": round(me_ms, 4),
-                     "achieved": round(dot4 / (me_ms * 1e-3) / 1e12, 2), "peak": round(DOT4_PEAK_T, 2),
-                     "unit": "T dot4 lane-ops/s", "frac": round(dot4 / (me_ms * 1e-3) / 1e12 / DOT4_PEAK_T, 4),
-                     "useful_dot4_per_launch": dot4,
+                     "achieved": round(issue / (me_ms * 1e-3) / 1e12, 4),
+                     "peak": round(ISSUE_PEAK_T, 4), "unit": "T SIMD issue-cycles/s",
+                     "frac": round(issue / (me_ms * 1e-3) / 1e12 / ISSUE_PEAK_T, 4),
+                     "issue_cycles_per_launch": issue, "tiles_per_launch": tiles,
+                     "per_tile": {"valu": ME_VALU_PER_TILE, "mfma": ME_MFMA_PER_TILE,
+                                  "source": "profiles/r05_pmc_me.json (SQ_INSTS_VALU - "
+                                            "SQ_INSTS_VALU_MFMA_I8, SQ_INSTS_MFMA per dispatch / tiles)"},
                      "mfma_i8": {"useful_TOPs": round(2 * macs / (me_ms * 1e-3) / 1e12, 1),
+                                 "live_TOPs": round(live_ops / (me_ms * 1e-3) / 1e12, 1),
                                  "peak_TOPs": MFMA_I8_PEAK_T,
-                                 "frac": round(2 * macs / (me_ms * 1e-3) / 1e12 / MFMA_I8_PEAK_T, 4)},
-                     "note": ("useful work = valid candidates x 64 px (SSD = sum c^2 + S2 - 2X); frac is "
-                              "the dot4-equivalent rate (candidates x 16 dot4 lane-ops against the "
-                              "half-rate dot4 VALU peak) so both search kernels share one scale; "
-                              + ("the matrix-core kernel computes 16 blocks (8 of two block rows) x 16 "
-                                 "window positions per MFMA and turns only the live result registers "
-                                 "into keys (DESIGN.md §5); it is neither MFMA- nor VALU-issue-bound "
-                                 "(mfma_i8.frac; PMC in profiles/)"
-                                 if mfma else "S2 pre-pass time included"))},
+                                 "frac_useful": round(2 * macs / (me_ms * 1e-3) / 1e12 / MFMA_I8_PEAK_T, 4),
+                                 "frac_live": round(live_ops / (me_ms * 1e-3) / 1e12 / MFMA_I8_PEAK_T, 4)},
+                     "note": ("frac = the kernel's VALU + MFMA issue cycles over the chip's issue "
+                              "capacity; the matrix cores run at mfma_i8.frac_live (all computed "
+                              "outputs, of which the block's 33 x 33 candidates are 34 %); "
+                              f"dot4-equivalent rate (valid candidates x 16 v_dot4 lane-ops against "
+                              f"the half-rate dot4 peak, the r02-r04 scale): "
+                              f"{dot4 / (me_ms * 1e-3) / 1e12 / DOT4_PEAK_T:.3f}")},
     }
     if verify is not None:
         torch.cuda.synchronize()

@@ -1304,20 +1304,17 @@ void fused_encode_kernel(FusedArgs a, QTab t) {
   typedef WaveLds<T, C, DUP, PST> L;
   __shared__ __attribute__((aligned(16))) unsigned char lds[4 * L::BYTES];
   __shared__ double srq[FAST ? 192 : 1];
-  // the table itself: staged for the division path (!FAST); the FAST path divides only in its
-  // rare exact fallback and reads the kernel argument there (1.5 KB less LDS: the C = 3
-  // encoder fits 8 workgroups per CU)
-  __shared__ D sq_lds[FAST ? 1 : 192];
-  const D* sq;
-  if constexpr (FAST) sq = t.q;
-  else sq = sq_lds;
+  // (the table itself, for the division path and the FAST path's exact fallback; read from the
+  // kernel argument instead, the 3-channel encoder measured 10 % slower: 0.4606 against
+  // 0.4198 ms, profiles/r05f_ab_cfg2.log, profiles/r05e_ab_cfg2.log)
+  __shared__ D sq[192];
   __shared__ uint32_t zh[OUTM == OUT_SYMH || OUTM == OUT_COEFH ? ZH_LDS : 1];
   const int tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
   const int b = lane >> 3, r = lane & 7;
   if (a.zr_gate && *a.zr_gate == 0) return;           // (the emitter's fallback, not needed)
   for (int i = tid; i < 192; i += 256) {
-    if constexpr (!FAST) sq_lds[i] = (D)t.q[i];
+    sq[i] = (D)t.q[i];
     // s_i * s_k * RN(1/q): the DCT's power-of-two output scales folded into the reciprocal
     // (1.0 / q is IEEE-correctly rounded here as on the host)
     if constexpr (FAST) srq[i] = (dct2_scale((i >> 3) & 7) * dct2_scale(i & 7)) * (1.0 / t.q[i]);

@@ -257,6 +257,8 @@ __device__ __forceinline__ void me2_search(const uint32_t* lds, int* red, int wa
     bri = min(bri, __builtin_amdgcn_update_dpp(INT_MAX, bri, 0x4E, 0xf, 0xf, false));
     bri = min(bri, __builtin_amdgcn_update_dpp(INT_MAX, bri, 0x141, 0xf, 0xf, false));
     bri = min(bri, __builtin_amdgcn_update_dpp(INT_MAX, bri, 0x140, 0xf, 0xf, false));
+    // (r05: letting a row's unique holder write its entry and reducing by DPP only on ties
+    // measured no faster, 4.679 against 4.663 ms, profiles/r05f_ab_me.log)
     if (l16 == 0) {
       const int blk = 8 * (i >> 1) + j;                  // tile block: row-major, 0..15
       red[2 * (wave * 16 + blk)] = best;

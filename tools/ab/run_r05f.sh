@@ -1,5 +1,6 @@
 #!/bin/bash
-# r05f: cfg2 A/B (one-tile prefetch + table out of LDS: 7 or 8 waves/SIMD), GPU tests, smoke,
+# r05f: cfg2 A/B (one-tile prefetch + table out of LDS: 7 or 8 waves/SIMD), ME A/B (single-holder
+# per-block reduction), GPU tests, smoke,
 # bench, tiny-call ubench
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -7,6 +8,8 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 600 python tools/ab/ab_cfg2.py ab/c3base.so ab/c3now.so ab/c3w8.so --rounds 4 --pace 0 > gpurun_out/r05f_ab_cfg2.log 2>&1 || { tail -20 gpurun_out/r05f_ab_cfg2.log; exit 1; }
 cat gpurun_out/r05f_ab_cfg2.log
+timeout -k 10 600 python tools/ab/ab_me.py ab/mebase.so ab/menow.so --rounds 4 --oracle > gpurun_out/r05f_ab_me.log 2>&1 || { tail -20 gpurun_out/r05f_ab_me.log; exit 1; }
+cat gpurun_out/r05f_ab_me.log
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r05f_pytest.log 2>&1 || { tail -40 gpurun_out/r05f_pytest.log; exit 1; }
 tail -3 gpurun_out/r05f_pytest.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r05f_smoke.log 2>&1 || { tail -20 gpurun_out/r05f_smoke.log; exit 1; }
