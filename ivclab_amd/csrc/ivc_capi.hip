@@ -171,6 +171,7 @@ struct DevCtx {
   void* tiny = nullptr;                     // page-locked, device-mapped block for tiny calls
   int tiny_state = 0;                       // 0 untried, 1 ready, -1 unavailable
   uint32_t tiny_seq = 0;                    // last completion value written behind a tiny call
+  uint32_t* tiny_count = nullptr;           // finished workgroups of the running tiny call
   void* slot[kSlots] = {};
   size_t cap[kSlots] = {};
   void* pin[kPinSlots] = {};
@@ -193,19 +194,17 @@ bool aux_ready(DevCtx* c) {
 }
 
 constexpr size_t kTinyMax = 64u << 10;      // bytes of input and of output for a tiny call
-// the completion word of a tiny call: written after everything before it on the stream
-__global__ void tiny_signal_kernel(uint32_t* flag, uint32_t seq) {
-  if (threadIdx.x == 0) {
-    __threadfence_system();
-    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
+
 // after the input and output blocks: the completion word a tiny call's stream writes
 constexpr size_t kTinyFlag = 2 * kTinyMax;
 bool tiny_ready(DevCtx* c) {
   if (c->tiny_state == 0) {
     c->tiny_state = hipHostMalloc(&c->tiny, 2 * kTinyMax + 256, hipHostMallocDefault) == hipSuccess ? 1 : -1;
     if (c->tiny_state == 1) *reinterpret_cast<volatile uint32_t*>((char*)c->tiny + kTinyFlag) = 0;
+    // the finished-workgroup counter of tiny_done (device memory, left at 0 by every call)
+    if (c->tiny_state == 1 && (hipMalloc((void**)&c->tiny_count, 4) != hipSuccess ||
+                               hipMemset(c->tiny_count, 0, 4) != hipSuccess))
+      c->tiny_state = -1;
     (void)hipGetLastError();
   }
   return c->tiny_state == 1;
@@ -382,11 +381,13 @@ struct Staging {
   // device addresses directly, the kernel reads it and writes its output there over the bus
   // (no DMA transfers to set up), then one sync and a copy out: one launch per call.
   // Returns false, nothing done, when the sizes do not qualify.
-  //   Completion: a one-wave kernel behind the op writes a sequence number into a page-locked
-  // word (system-scope release) and the host spins on it.  Per call (tools/ubench/tiny_call.hip,
-  // profiles/r05e_tiny_call.log): a blocking hipStreamSynchronize costs ~5 us more, and
-  // hipStreamWriteValue32 (a command-processor write) ~2.5 us more than the kernel.  The spin
-  // gives up after 50 ms and synchronises, which also reports a failed kernel.
+  //   Completion: the op's kernel itself — its last workgroup to finish (tiny_done,
+  // ivc_internal.h) — writes a sequence number into a page-locked word with a system-scope
+  // release, and the host spins on it.  Per call (tools/ubench/tiny_call.hip,
+  // profiles/r05_tiny_call.log): a blocking hipStreamSynchronize costs ~5 us more, a second
+  // one-wave kernel writing the word ~2 us more (the inter-kernel gap), hipStreamWriteValue32
+  // ~2.5 us more.  The spin gives up after 50 ms and synchronises, which also reports a failed
+  // kernel.
   template <typename L>
   bool tiny(const void* src, size_t IB, void* dst, size_t OB, const char* what, L&& launch) {
     if (status || IB > kTinyMax || OB > kTinyMax || !tiny_ready(ctx)) return false;
@@ -394,24 +395,19 @@ struct Staging {
     char* to = ti + kTinyMax;
     uint32_t* flag = reinterpret_cast<uint32_t*>(ti + kTinyFlag);
     if (IB) memcpy(ti, src, IB);
-    if (launched(launch(ti, to, ctx->stream), what)) return true;
     const uint32_t seq = ++ctx->tiny_seq;
+    const TinyDone td{flag, ctx->tiny_count, seq};
+    if (launched(launch(ti, to, ctx->stream, &td), what)) return true;
     bool done = false;
-    tiny_signal_kernel<<<1, 64, 0, ctx->stream>>>(flag, seq);
-    if (hipGetLastError() == hipSuccess) {
-      const auto t0 = std::chrono::steady_clock::now();
-      for (uint32_t i = 1;; ++i) {
-        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) {
-          done = true;
-          break;
-        }
-        __builtin_ia32_pause();
-        if ((i & 1023u) == 0 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
-          break;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+      if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) {
+        done = true;
+        break;
       }
-    } else {
-      (void)hipGetLastError();
+      __builtin_ia32_pause();
+      if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
+        break;
     }
     if (!done) {
       hipError_t e = hipStreamSynchronize(ctx->stream);
@@ -656,8 +652,8 @@ int ivc_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_
   TRY(st.open());
   const size_t ib = (size_t)nblk * 64 * dtype_size(src_dtype);
   const size_t ob = (size_t)nblk * 64 * dtype_size(dst_dtype);
-  if (st.tiny(src, ib, dst, ob, "dct8x8", [&](const void* i, void* o, hipStream_t s) {
-        return launch_dct8x8(i, src_dtype, nblk, o, dst_dtype, inverse, norm, s);
+  if (st.tiny(src, ib, dst, ob, "dct8x8", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
+        return launch_dct8x8(i, src_dtype, nblk, o, dst_dtype, inverse, norm, s, d);
       }))
     return st.status;
   if (st.pipelined(src, 64 * dtype_size(src_dtype), dst, 64 * dtype_size(dst_dtype), nblk, "dct8x8",
@@ -726,8 +722,8 @@ int ivc_quantize(const void* src, int src_dtype, int64_t nblk, int C, const doub
   Staging st;
   TRY(st.open());
   const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
-  if (st.tiny(src, ib, dst, ob, "quantize", [&](const void* i, void* o, hipStream_t s) {
-        return launch_quantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s);
+  if (st.tiny(src, ib, dst, ob, "quantize", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
+        return launch_quantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s, d);
       }))
     return st.status;
   if (st.pipelined(src, (size_t)C * 64 * dtype_size(src_dtype), dst, 192 * 4, nblk, "quantize",
@@ -763,8 +759,8 @@ int ivc_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const do
   Staging st;
   TRY(st.open());
   const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
-  if (st.tiny(src, ib, dst, ob, "dequantize", [&](const void* i, void* o, hipStream_t s) {
-        return launch_dequantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s);
+  if (st.tiny(src, ib, dst, ob, "dequantize", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
+        return launch_dequantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s, d);
       }))
     return st.status;
   if (st.pipelined(src, (size_t)C * 64 * dtype_size(src_dtype), dst, 192 * 4, nblk, "dequantize",
@@ -798,8 +794,8 @@ int ivc_zigzag(const void* src, int64_t nrow, int64_t stride, int esize, int inv
   Staging st;
   TRY(st.open());
   const size_t ib = (size_t)nrow * stride * esize, ob = (size_t)nrow * 64 * esize;
-  if (st.tiny(src, ib, dst, ob, "zigzag", [&](const void* i, void* o, hipStream_t s) {
-        return launch_zigzag(i, nrow, stride, esize, inverse, o, s);
+  if (st.tiny(src, ib, dst, ob, "zigzag", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
+        return launch_zigzag(i, nrow, stride, esize, inverse, o, s, d);
       }))
     return st.status;
   if (st.pipelined(src, (size_t)stride * esize, dst, 64 * (size_t)esize, nrow, "zigzag",

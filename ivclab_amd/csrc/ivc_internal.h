@@ -50,17 +50,41 @@ struct Error {
 int dtype_size(int dtype);
 bool dtype_is_float(int dtype);
 
+// Completion signal of a tiny host call (ivc_capi.hip): the last workgroup of the kernel to
+// finish — counted on `count` (device memory, left at 0) — stores `seq` into the page-locked
+// word `flag` with a system-scope release after every workgroup's writes are visible.  A null
+// `flag` (every other caller) adds nothing.
+struct TinyDone {
+  uint32_t* flag;
+  uint32_t* count;
+  uint32_t seq;
+};
+__device__ __forceinline__ void tiny_done(const TinyDone& d) {
+  if (d.flag == nullptr) return;                      // uniform
+  __threadfence_system();                             // this thread's writes, system scope
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t n = __hip_atomic_fetch_add(d.count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (n == gridDim.x - 1) {
+      __hip_atomic_store(d.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // all launchers enqueue on `s` and return hipSuccess / the launch error
 hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
-                         int inverse, int norm, hipStream_t s);
+                         int inverse, int norm, hipStream_t s, const TinyDone* done = nullptr);
 hipError_t launch_dct8x8_image(const void* img, int src_dtype, int64_t rows, int64_t W, int64_t C,
                                void* dst, int dst_dtype, int inverse, int norm, hipStream_t s);
 hipError_t launch_quantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
-                           int calc_dtype, int32_t* dst, hipStream_t s);
+                           int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done = nullptr);
 hipError_t launch_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
-                             int calc_dtype, int32_t* dst, hipStream_t s);
+                             int calc_dtype, int32_t* dst, hipStream_t s,
+                             const TinyDone* done = nullptr);
 hipError_t launch_zigzag(const void* src, int64_t nrow, int64_t stride, int esize, int inverse,
-                         void* dst, hipStream_t s);
+                         void* dst, hipStream_t s, const TinyDone* done = nullptr);
 // returns hipErrorInvalidValue for an unsupported dtype / C combination
 hipError_t launch_intra_encode(const void* img, int dtype, int64_t nframes, int64_t H, int64_t W,
                                int C, const QTab& t, int calc_dtype, int zigzag, int32_t* out,

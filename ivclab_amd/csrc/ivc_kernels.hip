@@ -106,7 +106,8 @@ struct ImgLayout {
 template <typename TI, typename T, bool INV, bool IMG = false>
 __global__ __launch_bounds__(256) void dct8x8_kernel(const TI* __restrict__ src, int64_t nunit,
                                                      T* __restrict__ dst, T fct, int ortho,
-                                                     ImgLayout im = ImgLayout{0, 1, 1}) {
+                                                     ImgLayout im = ImgLayout{0, 1, 1},
+                                                     TinyDone done = TinyDone{nullptr, nullptr, 0}) {
   __shared__ __attribute__((aligned(16))) T xs[32 * 72];
   const int tid = threadIdx.x, u = tid >> 3, r = tid & 7;
   for (int64_t g = blockIdx.x; g * 32 < nunit; g += gridDim.x) {
@@ -152,10 +153,13 @@ __global__ __launch_bounds__(256) void dct8x8_kernel(const TI* __restrict__ src,
       *reinterpret_cast<uint4*>(out + e) = *reinterpret_cast<const uint4*>(xs + e);
     __syncthreads();
   }
+  tiny_done(done);
 }
 
 hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
-                         int inverse, int norm, hipStream_t s) {
+                         int inverse, int norm, hipStream_t s, const TinyDone* done) {
+  const TinyDone dn = done ? *done : TinyDone{nullptr, nullptr, 0};
+  const ImgLayout im0{0, 1, 1};
   if (nblk <= 0) return hipSuccess;
   // scipy: inorm 0 -> fct 1, 1 (ortho) -> 1/sqrt(2N) = 1/4, 2 -> 1/(2N) = 1/16; the inverse
   // transform uses 2 - inorm (scipy/fft/_pocketfft/helper.py _normalization)
@@ -167,20 +171,20 @@ hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst
     if (src_dtype != IVC_F32) return hipErrorInvalidValue;
     if (inverse)
       dct8x8_kernel<float, float, true><<<grid, 256, 0, s>>>((const float*)src, nblk, (float*)dst,
-                                                              (float)fct, ortho);
+                                                              (float)fct, ortho, im0, dn);
     else
       dct8x8_kernel<float, float, false><<<grid, 256, 0, s>>>((const float*)src, nblk, (float*)dst,
-                                                               (float)fct, ortho);
+                                                               (float)fct, ortho, im0, dn);
     return hipGetLastError();
   }
   if (dst_dtype != IVC_F64 || src_dtype == IVC_F32) return hipErrorInvalidValue;
   IVC_DISPATCH_ALL(src_dtype, {
     if (inverse)
       dct8x8_kernel<TI, double, true><<<grid, 256, 0, s>>>((const TI*)src, nblk, (double*)dst,
-                                                           fct, ortho);
+                                                           fct, ortho, im0, dn);
     else
       dct8x8_kernel<TI, double, false><<<grid, 256, 0, s>>>((const TI*)src, nblk, (double*)dst,
-                                                            fct, ortho);
+                                                            fct, ortho, im0, dn);
   });
   return hipGetLastError();
 }
@@ -224,7 +228,8 @@ hipError_t launch_dct8x8_image(const void* img, int src_dtype, int64_t rows, int
 // ======================================================================================
 template <typename TI, typename D>
 __global__ __launch_bounds__(256) void quantize_kernel(const TI* __restrict__ src, int64_t nblk,
-                                                       int C, QTab t, int32_t* __restrict__ dst) {
+                                                       int C, QTab t, int32_t* __restrict__ dst,
+                                                       TinyDone done) {
   const int64_t total = nblk * 48;
   for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * 256) {
@@ -237,12 +242,13 @@ __global__ __launch_bounds__(256) void quantize_kernel(const TI* __restrict__ sr
       v[e] = np_to_i32<D>(rint_t<D>((D)sp[e] / (D)t.q[p * 64 + j + e]));
     *reinterpret_cast<int4*>(dst + g * 4) = make_int4(v[0], v[1], v[2], v[3]);
   }
+  tiny_done(done);
 }
 
 template <typename TI, typename D>
 __global__ __launch_bounds__(256) void dequantize_kernel(const TI* __restrict__ src,
                                                          int64_t nblk, int C, QTab t,
-                                                         int32_t* __restrict__ dst) {
+                                                         int32_t* __restrict__ dst, TinyDone done) {
   const int64_t total = nblk * 48;
   for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * 256) {
@@ -254,13 +260,15 @@ __global__ __launch_bounds__(256) void dequantize_kernel(const TI* __restrict__ 
     for (int e = 0; e < 4; ++e) v[e] = np_to_i32<D>((D)sp[e] * (D)t.q[p * 64 + j + e]);
     *reinterpret_cast<int4*>(dst + g * 4) = make_int4(v[0], v[1], v[2], v[3]);
   }
+  tiny_done(done);
 }
 
 template <bool DEQ>
 static hipError_t launch_quant_common(const void* src, int src_dtype, int64_t nblk, int C,
                                       const QTab& t, int calc_dtype, int32_t* dst,
-                                      hipStream_t s) {
+                                      hipStream_t s, const TinyDone* done) {
   if (nblk <= 0) return hipSuccess;
+  const TinyDone dn = done ? *done : TinyDone{nullptr, nullptr, 0};
   if (C != 1 && C != 3) return hipErrorInvalidValue;
   unsigned grid = grid_for(nblk * 48, 256, 16);
   if (calc_dtype == IVC_F32) {
@@ -269,17 +277,17 @@ static hipError_t launch_quant_common(const void* src, int src_dtype, int64_t nb
     IVC_DISPATCH_ALL(src_dtype, {
       if constexpr (sizeof(TI) <= 2 || std::is_same<TI, float>::value) {
         if (DEQ)
-          dequantize_kernel<TI, float><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst);
+          dequantize_kernel<TI, float><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
         else
-          quantize_kernel<TI, float><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst);
+          quantize_kernel<TI, float><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
       }
     });
   } else if (calc_dtype == IVC_F64) {
     IVC_DISPATCH_ALL(src_dtype, {
       if (DEQ)
-        dequantize_kernel<TI, double><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst);
+        dequantize_kernel<TI, double><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
       else
-        quantize_kernel<TI, double><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst);
+        quantize_kernel<TI, double><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
     });
   } else {
     return hipErrorInvalidValue;
@@ -288,12 +296,12 @@ static hipError_t launch_quant_common(const void* src, int src_dtype, int64_t nb
 }
 
 hipError_t launch_quantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
-                           int calc_dtype, int32_t* dst, hipStream_t s) {
-  return launch_quant_common<false>(src, src_dtype, nblk, C, t, calc_dtype, dst, s);
+                           int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done) {
+  return launch_quant_common<false>(src, src_dtype, nblk, C, t, calc_dtype, dst, s, done);
 }
 hipError_t launch_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
-                             int calc_dtype, int32_t* dst, hipStream_t s) {
-  return launch_quant_common<true>(src, src_dtype, nblk, C, t, calc_dtype, dst, s);
+                             int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done) {
+  return launch_quant_common<true>(src, src_dtype, nblk, C, t, calc_dtype, dst, s, done);
 }
 
 // ======================================================================================
@@ -303,7 +311,7 @@ hipError_t launch_dequantize(const void* src, int src_dtype, int64_t nblk, int C
 template <typename E>
 __global__ __launch_bounds__(256) void zigzag_kernel(const E* __restrict__ src, int64_t nrow,
                                                      int64_t stride, int inverse,
-                                                     E* __restrict__ dst) {
+                                                     E* __restrict__ dst, TinyDone done) {
   const int64_t total = nrow * 64;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * 256) {
@@ -311,17 +319,19 @@ __global__ __launch_bounds__(256) void zigzag_kernel(const E* __restrict__ src, 
     const int j = (int)(i & 63);
     dst[i] = src[row * stride + (inverse ? c_zz_order[j] : c_zz_scan[j])];
   }
+  tiny_done(done);
 }
 
 hipError_t launch_zigzag(const void* src, int64_t nrow, int64_t stride, int esize, int inverse,
-                         void* dst, hipStream_t s) {
+                         void* dst, hipStream_t s, const TinyDone* done) {
   if (nrow <= 0) return hipSuccess;
+  const TinyDone dn = done ? *done : TinyDone{nullptr, nullptr, 0};
   unsigned grid = grid_for(nrow * 64, 256, 16);
   switch (esize) {
-    case 1: zigzag_kernel<uint8_t><<<grid, 256, 0, s>>>((const uint8_t*)src, nrow, stride, inverse, (uint8_t*)dst); break;
-    case 2: zigzag_kernel<uint16_t><<<grid, 256, 0, s>>>((const uint16_t*)src, nrow, stride, inverse, (uint16_t*)dst); break;
-    case 4: zigzag_kernel<uint32_t><<<grid, 256, 0, s>>>((const uint32_t*)src, nrow, stride, inverse, (uint32_t*)dst); break;
-    case 8: zigzag_kernel<uint64_t><<<grid, 256, 0, s>>>((const uint64_t*)src, nrow, stride, inverse, (uint64_t*)dst); break;
+    case 1: zigzag_kernel<uint8_t><<<grid, 256, 0, s>>>((const uint8_t*)src, nrow, stride, inverse, (uint8_t*)dst, dn); break;
+    case 2: zigzag_kernel<uint16_t><<<grid, 256, 0, s>>>((const uint16_t*)src, nrow, stride, inverse, (uint16_t*)dst, dn); break;
+    case 4: zigzag_kernel<uint32_t><<<grid, 256, 0, s>>>((const uint32_t*)src, nrow, stride, inverse, (uint32_t*)dst, dn); break;
+    case 8: zigzag_kernel<uint64_t><<<grid, 256, 0, s>>>((const uint64_t*)src, nrow, stride, inverse, (uint64_t*)dst, dn); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
