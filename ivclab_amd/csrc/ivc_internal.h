@@ -64,6 +64,10 @@ __device__ __forceinline__ void tiny_done(const TinyDone& d) {
   __threadfence_system();                             // this thread's writes, system scope
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (gridDim.x == 1) {                             // the common tiny call: no counter
+      __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     const uint32_t n = __hip_atomic_fetch_add(d.count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (n == gridDim.x - 1) {
       __hip_atomic_store(d.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

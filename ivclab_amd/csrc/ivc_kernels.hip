@@ -441,6 +441,12 @@ struct FusedArgs {
 #ifndef IVC_C3_SPLIT
 #define IVC_C3_SPLIT 1         // C = 3 coefficients, small launches: one wave per (group, plane)
 #endif
+#ifndef IVC_COUNT_PREFETCH
+#define IVC_COUNT_PREFETCH IVC_PREFETCH   // the symbol count pass's load rounds
+#endif
+#ifndef IVC_COUNT_WAVES
+#define IVC_COUNT_WAVES 1      // the symbol count pass: min waves per SIMD (1: compiler's choice)
+#endif
 #ifndef IVC_C3_WAVES
 #define IVC_C3_WAVES 1         // C = 3 coefficients: min waves per SIMD the registers must allow
 #endif
@@ -1301,7 +1307,8 @@ __device__ __forceinline__ void coef_hist(const FusedArgs& a, const int32_t* os,
 template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SRC, bool CHECKMAG,
           int NG, bool DUP, int OUTM = OUT_COEFS>
 __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && C == 1 && DUP) ? 6
-                                  : (C == 3 && OUTM == OUT_COEFS ? IVC_C3_WAVES : 1))
+                                  : (C == 3 && OUTM == OUT_COEFS ? IVC_C3_WAVES
+                                     : (OUTM == OUT_COUNT ? IVC_COUNT_WAVES : 1)))
 void fused_encode_kernel(FusedArgs a, QTab t) {
   static_assert(OUTM == OUT_COEFS || OUTM == OUT_LUMA || OUTM == OUT_COEFH || (ZZ && SRC == SRC_IMAGE),
                 "symbols need zig-zag order");
@@ -1393,7 +1400,8 @@ void fused_encode_kernel(FusedArgs a, QTab t) {
 
   // (3-channel images: one tile ahead — the two-tile rounds measured slower there, 0.4266 vs
   // 0.4198 ms for 64 x 1080p RGB and 14.9 vs 8.7 us for one frame, profiles/r05e_ab_cfg2.log)
-  constexpr int PF = (SRC == SRC_IMAGE && TileRaw<TI, C, NG>::NW <= 8) ? (C == 3 ? 1 : IVC_PREFETCH) : 1;
+  constexpr int PF = (SRC == SRC_IMAGE && TileRaw<TI, C, NG>::NW <= 8)
+                        ? (C == 3 ? 1 : (OUTM == OUT_COUNT ? IVC_COUNT_PREFETCH : IVC_PREFETCH)) : 1;
   if (PST && a.split3) {
     // one wave per (group, plane): virtual unit vt = 3 lt + c; the group's rows are loaded
     // whole (the wave uses one channel of them) and its plane stored as soon as it is quantised

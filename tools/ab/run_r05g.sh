@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 600 python tools/ab/ab_cfg2.py ab/c3base.so ab/cur.so --rounds 4 --pace 0 > gpurun_out/r05g_ab_cfg2.log 2>&1 || { tail -20 gpurun_out/r05g_ab_cfg2.log; exit 1; }
 cat gpurun_out/r05g_ab_cfg2.log
-timeout -k 10 600 python tools/ab/ab_me.py ab/mebase.so ab/cur.so --rounds 4 --oracle > gpurun_out/r05g_ab_me.log 2>&1 || { tail -20 gpurun_out/r05g_ab_me.log; exit 1; }
+timeout -k 10 600 python tools/ab/ab_me.py ab/mebase.so ab/cur.so ab/mett.so --rounds 4 --oracle > gpurun_out/r05g_ab_me.log 2>&1 || { tail -20 gpurun_out/r05g_ab_me.log; exit 1; }
 cat gpurun_out/r05g_ab_me.log
 timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r05g_pytest.log 2>&1 || { tail -40 gpurun_out/r05g_pytest.log; exit 1; }
 tail -3 gpurun_out/r05g_pytest.log
