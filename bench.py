@@ -867,9 +867,12 @@ def leg_cfg2(args, dist, rank, world, dev, table, result, verify):
     frames = torch.randint(0, 256, (F, H, W, 3), device=dev, generator=g, dtype=torch.uint8)
     out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
     res = {}
-    for label, nf, reps in (("one_frame", 1, 200), (f"batch_{F}", F, 20)):
+    # (the batch warms up for ~0.1 s of back-to-back launches: after the launch-bound one-frame
+    # loop the first few dozen batch launches ran ~9 % slower than the steady state,
+    # profiles/r05g_ab_cfg2.log rounds 1 vs 2-4)
+    for label, nf, reps, warm in (("one_frame", 1, 200, 5), (f"batch_{F}", F, 40, 200)):
         fr, o = frames[:nf], out[:nf]
-        wall, ms = timed(dist, lambda: D.intra_encode(fr, table, o, zigzag=True), reps, 5)
+        wall, ms = timed(dist, lambda: D.intra_encode(fr, table, o, zigzag=True), reps, warm)
         algo = nf * H * W * 15
         res[label] = {"frames": nf, "ms_per_launch": round(ms, 4),
                       "Mpixels_per_s": round(world * nf * H * W * reps / wall / 1e6, 1),

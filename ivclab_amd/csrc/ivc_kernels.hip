@@ -442,11 +442,11 @@ struct FusedArgs {
 #define IVC_C3_SPLIT 1         // C = 3 coefficients, small launches: one wave per (group, plane)
 #endif
 #ifndef IVC_COUNT_PREFETCH
-#define IVC_COUNT_PREFETCH IVC_PREFETCH   // the symbol count pass's load rounds
-#endif
+#define IVC_COUNT_PREFETCH 1   // the symbol count pass: one tile ahead (2: 7.05 vs 6.96 ms for
+#endif                         // 256 x 4K pixels -> symbols, profiles/r05h_ab_symbols.log)
 #ifndef IVC_COUNT_WAVES
-#define IVC_COUNT_WAVES 1      // the symbol count pass: min waves per SIMD (1: compiler's choice)
-#endif
+#define IVC_COUNT_WAVES 7      // the symbol count pass: min waves per SIMD (1, the compiler's
+#endif                         // choice: 7.47 vs 7.27 ms with the histogram, r05i_ab_symbols.log)
 #ifndef IVC_C3_WAVES
 #define IVC_C3_WAVES 1         // C = 3 coefficients: min waves per SIMD the registers must allow
 #endif

@@ -29,6 +29,32 @@ __global__ void io_k(const uint8_t* in, double* out, unsigned* flag, unsigned se
   if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// the same with the input block passed by value in the kernel arguments (no device read of
+// host memory): 64 B of u8, and 512 B of float64
+struct Blk8 { uint8_t v[64]; };
+struct Blk64 { double v[64]; };
+__global__ void io_arg_k(Blk8 in, double* out, unsigned* flag, unsigned seq) {
+  const int t = threadIdx.x;
+  out[t] = (double)in.v[t] * 0.5;
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void io_arg64_k(Blk64 in, double* out, unsigned* flag, unsigned seq) {
+  const int t = threadIdx.x;
+  out[t] = in.v[t] * 0.5;
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void io64_k(const double* in, double* out, unsigned* flag, unsigned seq) {
+  const int t = threadIdx.x;
+  out[t] = in[t] * 0.5;
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -89,6 +115,32 @@ int main() {
     while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
   });
   (void)hipStreamSynchronize(s);
+  {
+    Blk8 b8;
+    memcpy(b8.v, min, 64);
+    run("launch io kernel, input in kernel args (64 B) + spin", [&](int) {
+      const unsigned q = ++seq;
+      b8.v[0] = (uint8_t)q;
+      io_arg_k<<<1, 64, 0, s>>>(b8, mout, flag, q);
+      while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+    });
+    (void)hipStreamSynchronize(s);
+    Blk64 b64;
+    for (int i = 0; i < 64; ++i) b64.v[i] = i;
+    run("launch io kernel, f64 input mapped (512 B) + spin", [&](int) {
+      const unsigned q = ++seq;
+      io64_k<<<1, 64, 0, s>>>((const double*)(min + 1024), mout, flag, q);
+      while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+    });
+    (void)hipStreamSynchronize(s);
+    run("launch io kernel, f64 input in kernel args (512 B) + spin", [&](int) {
+      const unsigned q = ++seq;
+      b64.v[0] = q;
+      io_arg64_k<<<1, 64, 0, s>>>(b64, mout, flag, q);
+      while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+    });
+    (void)hipStreamSynchronize(s);
+  }
   run("launch io kernel + hipStreamWriteValue32 + spin", [&](int) {
     const unsigned q = ++seq;
     io_k<<<1, 64, 0, s>>>(min, mout, flag + 16, q);
