@@ -377,9 +377,10 @@ struct Staging {
   }
   bool aux_used = false;
   // A tiny call (one 8x8 block, a (3, 8, 8) stack: the reference's per-block loops,
-  // exercises/ch3/E3-1_claude.py:47-60): the input is copied into a page-locked block the
-  // device addresses directly, the kernel reads it and writes its output there over the bus
-  // (no DMA transfers to set up), then one sync and a copy out: one launch per call.
+  // exercises/ch3/E3-1_claude.py:47-60): the input travels inside the kernel arguments (up
+  // to kTinyInline bytes; larger ones are copied into a page-locked block the device
+  // addresses directly), the kernel writes its output into page-locked memory over the bus
+  // (no DMA transfers to set up), then one wait and a copy out: one launch per call.
   // Returns false, nothing done, when the sizes do not qualify.
   //   Completion: the op's kernel itself — its last workgroup to finish (tiny_done,
   // ivc_internal.h) — writes a sequence number into a page-locked word with a system-scope
@@ -394,9 +395,14 @@ struct Staging {
     char* ti = (char*)ctx->tiny;
     char* to = ti + kTinyMax;
     uint32_t* flag = reinterpret_cast<uint32_t*>(ti + kTinyFlag);
-    if (IB) memcpy(ti, src, IB);
     const uint32_t seq = ++ctx->tiny_seq;
-    const TinyDone td{flag, ctx->tiny_count, seq};
+    TinyDone td{flag, ctx->tiny_count, seq};
+    if (IB <= (size_t)kTinyInline) {           // the input rides in the kernel arguments
+      td.inl = src;
+      td.inl_bytes = IB;
+    } else if (IB) {
+      memcpy(ti, src, IB);
+    }
     if (launched(launch(ti, to, ctx->stream, &td), what)) return true;
     bool done = false;
     const auto t0 = std::chrono::steady_clock::now();

@@ -4,6 +4,7 @@
 #include <mutex>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "../../include/ivc.h"
 
@@ -53,13 +54,50 @@ bool dtype_is_float(int dtype);
 // Completion signal of a tiny host call (ivc_capi.hip): the last workgroup of the kernel to
 // finish — counted on `count` (device memory, left at 0) — stores `seq` into the page-locked
 // word `flag` with a system-scope release after every workgroup's writes are visible.  A null
-// `flag` (every other caller) adds nothing.
+// `flag` (every other caller) adds nothing.  `inl` (host side only): the call's input, which
+// the launcher passes inside the kernel arguments (TinyIn<N>, N = the launcher's capacity)
+// when it fits: the kernel reads it from its argument segment instead of over the bus from
+// host memory (~1 us less per call, tools/ubench/tiny_call.hip, profiles/r05i_tiny_call.log;
+// each 512 B of arguments costs ~0.15 us of launch, so the capacity is sized per kernel).
+constexpr int kTinyInline = 1536;    // the largest capacity: a (3, 8, 8) float64 stack
 struct TinyDone {
   uint32_t* flag;
   uint32_t* count;
   uint32_t seq;
+  const void* inl = nullptr;
+  size_t inl_bytes = 0;
 };
-__device__ __forceinline__ void tiny_done(const TinyDone& d) {
+template <int N>
+struct TinyIn {
+  uint32_t* flag;
+  uint32_t* count;
+  uint32_t seq;
+  alignas(16) unsigned char in[N];
+};
+template <typename TD> struct IsTinyIn : std::false_type {};
+template <int N> struct IsTinyIn<TinyIn<N>> : std::true_type {};
+// launch f(TinyIn<N>) when the call's input travels in the arguments, else f(TinyDone);
+// f returns the launch status
+template <int N = kTinyInline, typename F>
+inline hipError_t with_tiny(const TinyDone* d, F&& f) {
+  if (d && d->inl && d->inl_bytes <= (size_t)N) {
+    TinyIn<N> t;
+    t.flag = d->flag;
+    t.count = d->count;
+    t.seq = d->seq;
+    __builtin_memcpy(t.in, d->inl, d->inl_bytes);
+    return f(t);
+  }
+  return f(d ? *d : TinyDone{nullptr, nullptr, 0});
+}
+// the kernel's input: the argument segment's copy for a TinyIn launch
+template <typename T, typename TD>
+__device__ __forceinline__ const T* tiny_src(const T* src, const TD& d) {
+  if constexpr (IsTinyIn<TD>::value) return reinterpret_cast<const T*>(d.in);
+  else return src;
+}
+template <typename TD>
+__device__ __forceinline__ void tiny_done(const TD& d) {
   if (d.flag == nullptr) return;                      // uniform
   __threadfence_system();                             // this thread's writes, system scope
   __syncthreads();

@@ -103,12 +103,13 @@ __device__ __forceinline__ void load8(const TI* __restrict__ p, TI* v) {
 struct ImgLayout {
   int64_t W, C, per_row;    // image width, channels, units per block row (W / 8 * C)
 };
-template <typename TI, typename T, bool INV, bool IMG = false>
+template <typename TI, typename T, bool INV, bool IMG = false, typename TD = TinyDone>
 __global__ __launch_bounds__(256) void dct8x8_kernel(const TI* __restrict__ src, int64_t nunit,
                                                      T* __restrict__ dst, T fct, int ortho,
                                                      ImgLayout im = ImgLayout{0, 1, 1},
-                                                     TinyDone done = TinyDone{nullptr, nullptr, 0}) {
+                                                     TD done = TD{}) {
   __shared__ __attribute__((aligned(16))) T xs[32 * 72];
+  src = tiny_src(src, done);
   const int tid = threadIdx.x, u = tid >> 3, r = tid & 7;
   for (int64_t g = blockIdx.x; g * 32 < nunit; g += gridDim.x) {
     const int64_t unit = g * 32 + u;
@@ -156,9 +157,37 @@ __global__ __launch_bounds__(256) void dct8x8_kernel(const TI* __restrict__ src,
   tiny_done(done);
 }
 
+// One block of a tiny host call (dct.transform(one (8, 8) block), the reference's per-block
+// loops): one wave, the input from the kernel arguments, rows on lanes 0..7, the transpose
+// through LDS with no workgroup barrier.  Same arithmetic as dct8x8_kernel.
+template <typename TI, typename T, bool INV>
+__global__ __launch_bounds__(64) void dct8x8_one_kernel(T* __restrict__ dst, T fct, int ortho,
+                                                        TinyIn<512> done) {
+  __shared__ __attribute__((aligned(16))) T xs[72];
+  const int r = threadIdx.x;
+  const TI* src = reinterpret_cast<const TI*>(done.in);
+  T x[8];
+  if (r < 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = (T)src[r * 8 + k];
+    if constexpr (INV) dct3_line<T>(x, fct, ortho != 0); else dct2_line<T>(x, fct, ortho != 0);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) xs[r * 9 + k] = x[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_s_waitcnt(0);
+  if (r < 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) x[i] = xs[i * 9 + r];
+    if constexpr (INV) dct3_line<T>(x, fct, ortho != 0); else dct2_line<T>(x, fct, ortho != 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) dst[i * 8 + r] = x[i];
+  }
+  tiny_done(done);
+}
+
 hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_dtype,
                          int inverse, int norm, hipStream_t s, const TinyDone* done) {
-  const TinyDone dn = done ? *done : TinyDone{nullptr, nullptr, 0};
   const ImgLayout im0{0, 1, 1};
   if (nblk <= 0) return hipSuccess;
   // scipy: inorm 0 -> fct 1, 1 (ortho) -> 1/sqrt(2N) = 1/4, 2 -> 1/(2N) = 1/16; the inverse
@@ -166,27 +195,57 @@ hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst
   int inorm = inverse ? 2 - norm : norm;
   double fct = inorm == 0 ? 1.0 : (inorm == 1 ? 0.25 : 0.0625);
   int ortho = norm == IVC_NORM_ORTHO;
+  if (nblk == 1 && done && done->inl && done->inl_bytes <= 512) {   // one block, tiny call
+    return with_tiny<512>(done, [&](auto dn) -> hipError_t {
+      if constexpr (IsTinyIn<decltype(dn)>::value) {
+        if (dst_dtype == IVC_F32) {
+          if (src_dtype != IVC_F32) return hipErrorInvalidValue;
+          if (inverse)
+            dct8x8_one_kernel<float, float, true><<<1, 64, 0, s>>>((float*)dst, (float)fct, ortho, dn);
+          else
+            dct8x8_one_kernel<float, float, false><<<1, 64, 0, s>>>((float*)dst, (float)fct, ortho, dn);
+          return hipGetLastError();
+        }
+        if (dst_dtype != IVC_F64 || src_dtype == IVC_F32) return hipErrorInvalidValue;
+        IVC_DISPATCH_ALL(src_dtype, {
+          if (inverse)
+            dct8x8_one_kernel<TI, double, true><<<1, 64, 0, s>>>((double*)dst, fct, ortho, dn);
+          else
+            dct8x8_one_kernel<TI, double, false><<<1, 64, 0, s>>>((double*)dst, fct, ortho, dn);
+        });
+        return hipGetLastError();
+      } else {
+        return hipErrorInvalidValue;              // (unreachable: the input fits)
+      }
+    });
+  }
   unsigned grid = grid_for(nblk, 32, 8);
   if (dst_dtype == IVC_F32) {
     if (src_dtype != IVC_F32) return hipErrorInvalidValue;
-    if (inverse)
-      dct8x8_kernel<float, float, true><<<grid, 256, 0, s>>>((const float*)src, nblk, (float*)dst,
-                                                              (float)fct, ortho, im0, dn);
-    else
-      dct8x8_kernel<float, float, false><<<grid, 256, 0, s>>>((const float*)src, nblk, (float*)dst,
-                                                               (float)fct, ortho, im0, dn);
-    return hipGetLastError();
+    return with_tiny(done, [&](auto dn) -> hipError_t {
+      using TD = decltype(dn);
+      if (inverse)
+        dct8x8_kernel<float, float, true, false, TD><<<grid, 256, 0, s>>>(
+            (const float*)src, nblk, (float*)dst, (float)fct, ortho, im0, dn);
+      else
+        dct8x8_kernel<float, float, false, false, TD><<<grid, 256, 0, s>>>(
+            (const float*)src, nblk, (float*)dst, (float)fct, ortho, im0, dn);
+      return hipGetLastError();
+    });
   }
   if (dst_dtype != IVC_F64 || src_dtype == IVC_F32) return hipErrorInvalidValue;
-  IVC_DISPATCH_ALL(src_dtype, {
-    if (inverse)
-      dct8x8_kernel<TI, double, true><<<grid, 256, 0, s>>>((const TI*)src, nblk, (double*)dst,
-                                                           fct, ortho, im0, dn);
-    else
-      dct8x8_kernel<TI, double, false><<<grid, 256, 0, s>>>((const TI*)src, nblk, (double*)dst,
-                                                            fct, ortho, im0, dn);
+  return with_tiny(done, [&](auto dn) -> hipError_t {
+    using TD = decltype(dn);
+    IVC_DISPATCH_ALL(src_dtype, {
+      if (inverse)
+        dct8x8_kernel<TI, double, true, false, TD><<<grid, 256, 0, s>>>(
+            (const TI*)src, nblk, (double*)dst, fct, ortho, im0, dn);
+      else
+        dct8x8_kernel<TI, double, false, false, TD><<<grid, 256, 0, s>>>(
+            (const TI*)src, nblk, (double*)dst, fct, ortho, im0, dn);
+    });
+    return hipGetLastError();
   });
-  return hipGetLastError();
 }
 
 // DCT of the Patcher view of `rows` block rows of an [., W, C] image (dct.py:12-46 on
@@ -226,13 +285,14 @@ hipError_t launch_dct8x8_image(const void* img, int src_dtype, int64_t rows, int
 // Quantise / dequantise (patchquant.py:44-78).  Element-wise over the [blk][3][64] output,
 // 4 outputs (one 16-byte store) per thread; C = 1 inputs broadcast over the 3 planes.
 // ======================================================================================
-template <typename TI, typename D>
+template <typename TI, typename D, typename TD>
 __global__ __launch_bounds__(256) void quantize_kernel(const TI* __restrict__ src, int64_t nblk,
                                                        int C, QTab t, int32_t* __restrict__ dst,
-                                                       TinyDone done) {
+                                                       TD done) {
+  src = tiny_src(src, done);
   const int64_t total = nblk * 48;
-  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < total;
-       g += (int64_t)gridDim.x * 256) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t blk = g / 48;
     const int o = (int)(g - blk * 48) * 4, p = o >> 6, j = o & 63;
     const TI* sp = src + (blk * C + (C == 1 ? 0 : p)) * 64 + j;
@@ -245,13 +305,14 @@ __global__ __launch_bounds__(256) void quantize_kernel(const TI* __restrict__ sr
   tiny_done(done);
 }
 
-template <typename TI, typename D>
+template <typename TI, typename D, typename TD>
 __global__ __launch_bounds__(256) void dequantize_kernel(const TI* __restrict__ src,
                                                          int64_t nblk, int C, QTab t,
-                                                         int32_t* __restrict__ dst, TinyDone done) {
+                                                         int32_t* __restrict__ dst, TD done) {
+  src = tiny_src(src, done);
   const int64_t total = nblk * 48;
-  for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < total;
-       g += (int64_t)gridDim.x * 256) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
+       g += (int64_t)gridDim.x * blockDim.x) {
     const int64_t blk = g / 48;
     const int o = (int)(g - blk * 48) * 4, p = o >> 6, j = o & 63;
     const TI* sp = src + (blk * C + (C == 1 ? 0 : p)) * 64 + j;
@@ -268,31 +329,39 @@ static hipError_t launch_quant_common(const void* src, int src_dtype, int64_t nb
                                       const QTab& t, int calc_dtype, int32_t* dst,
                                       hipStream_t s, const TinyDone* done) {
   if (nblk <= 0) return hipSuccess;
-  const TinyDone dn = done ? *done : TinyDone{nullptr, nullptr, 0};
   if (C != 1 && C != 3) return hipErrorInvalidValue;
   unsigned grid = grid_for(nblk * 48, 256, 16);
+  // one (3, 8, 8) stack (a tiny host call): one wave, not four
+  const unsigned nt = nblk * 48 <= 64 ? 64 : 256;
   if (calc_dtype == IVC_F32) {
     // float32 arithmetic only arises for float32 or <= 16-bit integer inputs
     if (dtype_size(src_dtype) > 2 && src_dtype != IVC_F32) return hipErrorInvalidValue;
-    IVC_DISPATCH_ALL(src_dtype, {
-      if constexpr (sizeof(TI) <= 2 || std::is_same<TI, float>::value) {
-        if (DEQ)
-          dequantize_kernel<TI, float><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
-        else
-          quantize_kernel<TI, float><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
-      }
+    return with_tiny(done, [&](auto dn) -> hipError_t {
+      using TD = decltype(dn);
+      IVC_DISPATCH_ALL(src_dtype, {
+        if constexpr (sizeof(TI) <= 2 || std::is_same<TI, float>::value) {
+          if (DEQ)
+            dequantize_kernel<TI, float, TD><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
+          else
+            quantize_kernel<TI, float, TD><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
+        }
+      });
+      return hipGetLastError();
     });
-  } else if (calc_dtype == IVC_F64) {
-    IVC_DISPATCH_ALL(src_dtype, {
-      if (DEQ)
-        dequantize_kernel<TI, double><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
-      else
-        quantize_kernel<TI, double><<<grid, 256, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
-    });
-  } else {
-    return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  if (calc_dtype == IVC_F64) {
+    return with_tiny(done, [&](auto dn) -> hipError_t {
+      using TD = decltype(dn);
+      IVC_DISPATCH_ALL(src_dtype, {
+        if (DEQ)
+          dequantize_kernel<TI, double, TD><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
+        else
+          quantize_kernel<TI, double, TD><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
+      });
+      return hipGetLastError();
+    });
+  }
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_quantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
@@ -308,13 +377,14 @@ hipError_t launch_dequantize(const void* src, int src_dtype, int64_t nblk, int C
 // Zig-zag permutation of 64-element rows (shape.py:21-36): flatten dst[j] = src[scan[j]]
 // (the inverse of the reference's scatter by zigzag_order), unflatten dst[j] = src[order[j]].
 // ======================================================================================
-template <typename E>
+template <typename E, typename TD>
 __global__ __launch_bounds__(256) void zigzag_kernel(const E* __restrict__ src, int64_t nrow,
                                                      int64_t stride, int inverse,
-                                                     E* __restrict__ dst, TinyDone done) {
+                                                     E* __restrict__ dst, TD done) {
+  src = tiny_src(src, done);
   const int64_t total = nrow * 64;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = i >> 6;
     const int j = (int)(i & 63);
     dst[i] = src[row * stride + (inverse ? c_zz_order[j] : c_zz_scan[j])];
@@ -325,16 +395,19 @@ __global__ __launch_bounds__(256) void zigzag_kernel(const E* __restrict__ src, 
 hipError_t launch_zigzag(const void* src, int64_t nrow, int64_t stride, int esize, int inverse,
                          void* dst, hipStream_t s, const TinyDone* done) {
   if (nrow <= 0) return hipSuccess;
-  const TinyDone dn = done ? *done : TinyDone{nullptr, nullptr, 0};
   unsigned grid = grid_for(nrow * 64, 256, 16);
-  switch (esize) {
-    case 1: zigzag_kernel<uint8_t><<<grid, 256, 0, s>>>((const uint8_t*)src, nrow, stride, inverse, (uint8_t*)dst, dn); break;
-    case 2: zigzag_kernel<uint16_t><<<grid, 256, 0, s>>>((const uint16_t*)src, nrow, stride, inverse, (uint16_t*)dst, dn); break;
-    case 4: zigzag_kernel<uint32_t><<<grid, 256, 0, s>>>((const uint32_t*)src, nrow, stride, inverse, (uint32_t*)dst, dn); break;
-    case 8: zigzag_kernel<uint64_t><<<grid, 256, 0, s>>>((const uint64_t*)src, nrow, stride, inverse, (uint64_t*)dst, dn); break;
-    default: return hipErrorInvalidValue;
-  }
-  return hipGetLastError();
+  const unsigned nt = nrow <= 4 ? 64 : 256;    // a tiny call's few rows: one wave
+  if (esize != 1 && esize != 2 && esize != 4 && esize != 8) return hipErrorInvalidValue;
+  return with_tiny(done, [&](auto dn) -> hipError_t {
+    using TD = decltype(dn);
+    switch (esize) {
+      case 1: zigzag_kernel<uint8_t, TD><<<grid, nt, 0, s>>>((const uint8_t*)src, nrow, stride, inverse, (uint8_t*)dst, dn); break;
+      case 2: zigzag_kernel<uint16_t, TD><<<grid, nt, 0, s>>>((const uint16_t*)src, nrow, stride, inverse, (uint16_t*)dst, dn); break;
+      case 4: zigzag_kernel<uint32_t, TD><<<grid, nt, 0, s>>>((const uint32_t*)src, nrow, stride, inverse, (uint32_t*)dst, dn); break;
+      default: zigzag_kernel<uint64_t, TD><<<grid, nt, 0, s>>>((const uint64_t*)src, nrow, stride, inverse, (uint64_t*)dst, dn); break;
+    }
+    return hipGetLastError();
+  });
 }
 
 // ======================================================================================
@@ -1308,7 +1381,7 @@ template <typename TI, typename T, typename D, int C, bool FAST, bool ZZ, int SR
           int NG, bool DUP, int OUTM = OUT_COEFS>
 __global__ __launch_bounds__(256, ((OUTM == OUT_SYMH || OUTM == OUT_SYMBOLS) && C == 1 && DUP) ? 6
                                   : (C == 3 && OUTM == OUT_COEFS ? IVC_C3_WAVES
-                                     : (OUTM == OUT_COUNT ? IVC_COUNT_WAVES : 1)))
+                                     : (OUTM == OUT_COUNT && C == 1 ? IVC_COUNT_WAVES : 1)))
 void fused_encode_kernel(FusedArgs a, QTab t) {
   static_assert(OUTM == OUT_COEFS || OUTM == OUT_LUMA || OUTM == OUT_COEFH || (ZZ && SRC == SRC_IMAGE),
                 "symbols need zig-zag order");

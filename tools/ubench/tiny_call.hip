@@ -55,6 +55,24 @@ __global__ void io64_k(const double* in, double* out, unsigned* flag, unsigned s
   if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// the same, completion without the system fence: each lane's payload store is a system-scope
+// (sc0 sc1) store, the wave waits for its stores (vmcnt 0), then lane 0 stores the flag
+__global__ void io_arg_nofence_k(Blk64 in, double* out, unsigned* flag, unsigned seq) {
+  const int t = threadIdx.x;
+  __hip_atomic_store(out + t, in.v[t] * 0.5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_s_waitcnt(0);
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// 4 waves, with the system fence (the library's op kernels are 256 threads)
+__global__ void io_arg_256_k(Blk64 in, double* out, unsigned* flag, unsigned seq) {
+  const int t = threadIdx.x;
+  if (t < 64) out[t] = in.v[t] * 0.5;
+  __threadfence_system();
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 static double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -75,6 +93,7 @@ static void run(const char* name, F&& f, int n = 3000) {
 }
 
 int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);   // a crash keeps the lines before it
   hipStream_t s;
   (void)hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   hipEvent_t ev;
@@ -140,6 +159,22 @@ int main() {
       while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
     });
     (void)hipStreamSynchronize(s);
+    run("  same, 256 threads", [&](int) {
+      const unsigned q = ++seq;
+      b64.v[0] = q;
+      io_arg_256_k<<<1, 256, 0, s>>>(b64, mout, flag, q);
+      while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+    });
+    (void)hipStreamSynchronize(s);
+    run("  same, 64 threads, no fence (sc1 stores + vmcnt(0))", [&](int) {
+      const unsigned q = ++seq;
+      b64.v[0] = q;
+      io_arg_nofence_k<<<1, 64, 0, s>>>(b64, mout, flag, q);
+      while (__atomic_load_n(flag, __ATOMIC_ACQUIRE) != q) __builtin_ia32_pause();
+    });
+    (void)hipStreamSynchronize(s);
+    for (int i = 0; i < 64; ++i)
+      if (mout[i] != (i ? i * 0.5 : b64.v[0] * 0.5)) { printf("nofence: out[%d] = %g\n", i, mout[i]); break; }
   }
   run("launch io kernel + hipStreamWriteValue32 + spin", [&](int) {
     const unsigned q = ++seq;
