@@ -28,7 +28,25 @@ _CHROM = np.asarray([
 
 
 _SCALAR_TYPES = (float, int, np.float64, np.float32, np.float16)
-_CALC = {}                       # (input dtype, table dtype) -> ivc code of NumPy's result dtype (0: none)
+_FAST = {}                       # (input dtype, shape, table dtype) -> _fast_args(...)
+
+
+def _fast_args(dt, shape, tdt):
+    """(dtype code, C, output shape, arithmetic code) of a fast-path call, or None when the
+    general path must run (a non-kernel dtype, broadcasting block axes, an empty array, or
+    arithmetic NumPy would not do in float32/float64)."""
+    code = N.DTYPE_CODE.get(dt)
+    if code is None or len(shape) < 2 or shape[-2:] != (8, 8) or 0 in shape:
+        return None
+    if len(shape) > 2 and shape[-3] not in (1, 3):
+        return None
+    calc = np.result_type(dt, tdt)
+    if calc not in (np.float32, np.float64):
+        return None
+    C = 1 if len(shape) == 2 else shape[-3]
+    lead = tuple(shape[:-3]) + (3, 8, 8)
+    oshape = (1,) * (5 - len(lead)) + lead if len(lead) < 5 else lead
+    return code, C, oshape, N.DTYPE_CODE[calc]
 
 
 def _as_blocks(x: np.ndarray, table: np.ndarray):
@@ -78,43 +96,39 @@ class PatchQuant:
         change (compared by value: the reference rebuilds the table per call, and a caller may
         edit luminance / chrominance in place)."""
         lum, chrom, sc = self.luminance, self.chrominance, self.quantization_scale
-        if type(lum) is np.ndarray and type(chrom) is np.ndarray and type(sc) in _SCALAR_TYPES:
-            key = (lum.dtype.str, lum.shape, lum.tobytes(), chrom.dtype.str, chrom.shape,
-                   chrom.tobytes(), type(sc), sc)
-            c = self.__dict__.get("_tcache")
-            if c is not None and c[0] == key:
-                return c[1], c[2], c[3]
-        else:
-            key = None
+        c = self.__dict__.get("_tcache")
+        # the same array objects with the same shape, dtype and bytes, and the same scale
+        if c is not None and lum is c[0] and chrom is c[1] and type(lum) is np.ndarray \
+                and type(chrom) is np.ndarray and type(sc) is c[3] and sc == c[2] \
+                and lum.shape == c[4] and chrom.shape == c[5] and lum.dtype is c[6] \
+                and chrom.dtype is c[7] and lum.tobytes() == c[8] and chrom.tobytes() == c[9]:
+            return c[10], c[11], c[12]
         table = np.asarray(self.get_quantization_table())
         targ = N.table_arg(table) if table.shape == (3, 8, 8) else None
         tptr = N.ptr(targ) if targ is not None else None
-        if key is not None:
-            self.__dict__["_tcache"] = (key, table, targ, tptr)
+        if type(lum) is np.ndarray and type(chrom) is np.ndarray and type(sc) in _SCALAR_TYPES:
+            self.__dict__["_tcache"] = (lum, chrom, sc, type(sc), lum.shape, chrom.shape, lum.dtype,
+                                        chrom.dtype, lum.tobytes(), chrom.tobytes(), table, targ, tptr)
         return table, targ, tptr
 
     def _run(self, x, entry: str, what: str):
         # fast path (the reference's per-block loops: one (3, 8, 8) or (8, 8) call per block):
-        # a C-contiguous array of a kernel dtype whose block axes need no broadcasting
-        if type(x) is np.ndarray and x.shape[-2:] == (8, 8) \
-                and (x.ndim == 2 or x.shape[-3] in (1, 3)) and 0 < x.size <= 12288:
-            code = N.DTYPE_CODE.get(x.dtype)
-            if code is not None:
+        # a C-contiguous array of a kernel dtype whose block axes need no broadcasting; the
+        # per-(dtype, shape) launch arguments are cached
+        if type(x) is np.ndarray and x.size <= 12288:
+            table, targ, tptr = self._table_args()
+            fk = (x.dtype, x.shape, table.dtype)
+            f = _FAST.get(fk)
+            if f is None:
+                f = _FAST[fk] = _fast_args(x.dtype, x.shape, table.dtype)
+            if f and targ is not None:
                 if not x.flags.c_contiguous:
                     x = np.ascontiguousarray(x)
-                table, targ, tptr = self._table_args()
-                ck = (x.dtype, table.dtype)
-                cc = _CALC.get(ck)
-                if cc is None:
-                    calc = np.result_type(x.dtype, table.dtype)
-                    cc = _CALC[ck] = N.DTYPE_CODE[calc] if calc in (np.float32, np.float64) else 0
-                if targ is not None and cc:
-                    C = 1 if x.ndim == 2 else x.shape[-3]
-                    lead = x.shape[:-3] + (3, 8, 8)
-                    out = np.empty((1,) * (5 - len(lead)) + lead if len(lead) < 5 else lead, np.int32)
-                    N.check(getattr(N.lib(), entry)(N.ptr(x), code, out.size // 192, C, tptr, cc,
-                                                    N.ptr(out)), what)
-                    return out
+                code, C, oshape, cc = f
+                out = np.empty(oshape, np.int32)
+                N.check(getattr(N.lib(), entry)(N.ptr(x), code, out.size // 192, C, tptr, cc,
+                                                N.ptr(out)), what)
+                return out
         x = np.asarray(x)
         table = np.asarray(self.get_quantization_table())
         if table.shape != (3, 8, 8):
