@@ -48,9 +48,6 @@ constexpr int MASK_C = -(1 << 22);               // C of a (block, window) pair 
 
 typedef int mf_v4i __attribute__((ext_vector_type(4)));
 typedef unsigned int mf_u32x2 __attribute__((ext_vector_type(2)));
-#ifndef IVC_ME_PAIR
-#define IVC_ME_PAIR 0
-#endif
 
 // ---- two block rows per tile --------------------------------------------------
 // A tile is 8 adjacent blocks of block row by (top) and the 8 below them (bottom): 16 MFMA
@@ -139,102 +136,14 @@ __device__ __forceinline__ void me2_search(const uint32_t* lds, int* red, int wa
       if (bot && q23) acc[3] = max(acc[3], (int)(((uint32_t)d.w << 8) + e));
     }
   };
-  // IVC_ME_PAIR: the two M-tiles of a segment as two independent MFMA chains interleaved step
-  // by step (each step's row and energy reads issued a step ahead), so one chain's MFMA covers
-  // the other's result latency and the keys of both fold into one v_max3 per register.  The
-  // steps go in a rolled loop of step pairs (even offset: block operand bop, odd: bks) — fully
-  // unrolled, the scheduler's hoisting spills
-  auto mpair = [&](int mt0, auto q01c, auto q23c) {
-    constexpr bool q01 = decltype(q01c)::value, q23 = decltype(q23c)::value;
-    // (opaque to the optimiser: what derives from mt0 — masks, addresses — is then formed here,
-    // not hoisted out of the tile loop to stay live through the staging and energy phases)
-    asm volatile("" : "+s"(mt0));
-    const int wd = 4 * mt0 + (l16 >> 2);
-    const int v0 = 16 * mt0 + l16 - 8 * g, v1 = v0 - 32, v2 = v0 + 16, v3 = v1 + 16;
-    const int c0 = (unsigned)v0 <= 32u ? 0 : MASK_C, c1 = (unsigned)v1 <= 32u ? 0 : MASK_C;
-    const int c2 = (unsigned)v2 <= 32u ? 0 : MASK_C, c3 = (unsigned)v3 <= 32u ? 0 : MASK_C;
-    const mf_v4i cmA = mf_v4i{c0, c1, c0, c1}, cmB = mf_v4i{c2, c3, c2, c3};
-    const uint32_t* rb = cb + (r0 + 2 * g) * PITCH + wd;   // row kk: rb + kk * PITCH
-    const int* em = ev + 16 * mt0;                          // offset dl: em + dl * U
-    mf_v4i TA, TB;
-    TA = mf_v4i{(int)rb[0], (int)rb[1], (int)rb[PITCH], (int)rb[PITCH + 1]};
-    TB = mf_v4i{(int)rb[4], (int)rb[5], (int)rb[PITCH + 4], (int)rb[PITCH + 5]};
-    int eA = em[0], eB = em[16];
-    // one step at offset dl (ODD: dl odd); `more`: a step follows (its row and energies are read)
-    auto step = [&](int dl, auto oddc, auto topc, auto botc, bool more) {
-      constexpr bool ODD = decltype(oddc)::value;
-      constexpr bool top = decltype(topc)::value, bot = decltype(botc)::value;
-      mf_u32x2 nA = {0u, 0u}, nB = {0u, 0u};
-      int neA = 0, neB = 0;
-      if (more) {
-        const uint32_t* p = rb + (dl + 2) * PITCH;
-        nA = mf_u32x2{p[0], p[1]};
-        nB = mf_u32x2{p[4], p[5]};
-        neA = em[(dl + 1) * U];
-        neB = em[(dl + 1) * U + 16];
-      }
-      const mf_v4i bo = ODD ? bks : bop;
-      const mf_v4i dA = __builtin_amdgcn_mfma_i32_16x16x64_i8(bo, TA, cmA, 0, 0, 0);
-      const mf_v4i dB = __builtin_amdgcn_mfma_i32_16x16x64_i8(bo, TB, cmB, 0, 0, 0);
-      const uint32_t ea = (uint32_t)eA, eb = (uint32_t)eB;
-      auto k2 = [&](int i, int x, int y) {
-        acc[i] = max(acc[i], max((int)(((uint32_t)x << 8) + ea), (int)(((uint32_t)y << 8) + eb)));
-      };
-      if (top && q01) k2(0, dA.x, dB.x);
-      if (top && q23) k2(1, dA.y, dB.y);
-      if (bot && q01) k2(2, dA.z, dB.z);
-      if (bot && q23) k2(3, dA.w, dB.w);
-      // the next step uses rows (dl + 1, dl + 2): row dl + 2 replaces row dl's half
-      if (ODD) {
-        TA.z = (int)nA.x; TA.w = (int)nA.y;
-        TB.z = (int)nB.x; TB.w = (int)nB.y;
-      } else {
-        TA.x = (int)nA.x; TA.y = (int)nA.y;
-        TB.x = (int)nB.x; TB.y = (int)nB.y;
-      }
-      eA = neA;
-      eB = neB;
-    };
-    using T_ = std::true_type;
-    using F_ = std::false_type;
-    // R = r0 + dl: top blocks live for R <= 32, bottom for R >= 8
-    if constexpr (WV == 0) {          // R 0..10: bottom from dl = 8
+  // (the two M-tiles of a segment as two interleaved MFMA chains were measured slower: the
+  // extra registers spill at 128 VGPRs)
 #pragma unroll 1
-      for (int dl = 0; dl < 8; dl += 2) {
-        step(dl, F_{}, T_{}, F_{}, true);
-        step(dl + 1, T_{}, T_{}, F_{}, true);
-      }
-      step(8, F_{}, T_{}, T_{}, true);
-      step(9, T_{}, T_{}, T_{}, true);
-      step(10, F_{}, T_{}, T_{}, false);
-    } else if constexpr (WV == 3) {   // R 31..40: top only at dl 0, 1
-      step(0, F_{}, T_{}, T_{}, true);
-      step(1, T_{}, T_{}, T_{}, true);
+  for (int mt = 0; mt < 2; ++mt) mtile(mt, std::true_type{}, std::false_type{});
 #pragma unroll 1
-      for (int dl = 2; dl < 10; dl += 2) {
-        step(dl, F_{}, F_{}, T_{}, true);
-        step(dl + 1, T_{}, F_{}, T_{}, dl + 2 < 10);
-      }
-    } else {                          // R 11..30 / 21..30: both
+  for (int mt = 2; mt < 4; ++mt) mtile(mt, std::true_type{}, std::true_type{});
 #pragma unroll 1
-      for (int dl = 0; dl < 10; dl += 2) {
-        step(dl, F_{}, T_{}, T_{}, true);
-        step(dl + 1, T_{}, T_{}, T_{}, dl + 2 < 10);
-      }
-    }
-  };
-  if constexpr (IVC_ME_PAIR) {
-    mpair(0, std::true_type{}, std::false_type{});
-    mpair(2, std::true_type{}, std::true_type{});
-    mpair(4, std::false_type{}, std::true_type{});
-  } else {
-#pragma unroll 1
-    for (int mt = 0; mt < 2; ++mt) mtile(mt, std::true_type{}, std::false_type{});
-#pragma unroll 1
-    for (int mt = 2; mt < 4; ++mt) mtile(mt, std::true_type{}, std::true_type{});
-#pragma unroll 1
-    for (int mt = 4; mt < NMT; ++mt) mtile(mt, std::false_type{}, std::true_type{});
-  }
+  for (int mt = 4; mt < NMT; ++mt) mtile(mt, std::false_type{}, std::true_type{});
   // per block: best -K' over the 16 lanes, then the least raster index among its holders
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
