@@ -174,6 +174,34 @@ def lib():
     return L
 
 
+_fast = False          # False: not tried yet; None: unavailable
+
+
+def fast():
+    """The per-block call accelerator (ivc_pyfast.c: the small-array fast paths of
+    DiscreteCosineTransform and PatchQuant in one C step), bound to this process's libivc
+    entry points after the device check; None when its module is missing (the ctypes path then
+    serves those calls)."""
+    global _fast
+    if _fast is False:
+        L = lib()
+        try:
+            import importlib.machinery
+            import importlib.util
+            import sysconfig
+            path = os.path.join(_HERE, "_lib", "_ivcfast" + sysconfig.get_config_var("EXT_SUFFIX"))
+            loader = importlib.machinery.ExtensionFileLoader("ivclab_amd._ivcfast", path)
+            spec = importlib.util.spec_from_file_location("ivclab_amd._ivcfast", path, loader=loader)
+            mod = importlib.util.module_from_spec(spec)
+            loader.exec_module(mod)
+            addr = lambda f: _ct.cast(f, _ct.c_void_p).value  # noqa: E731
+            mod.set_entry_points(addr(L.ivc_dct8x8), addr(L.ivc_quantize), addr(L.ivc_dequantize))
+            _fast = mod
+        except (ImportError, OSError):
+            _fast = None
+    return _fast
+
+
 def check(status: int, what: str = "ivc") -> None:
     """Map a libivc status to the exception class NumPy would raise for the same misuse."""
     if status == 0:

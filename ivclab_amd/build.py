@@ -46,9 +46,41 @@ def _run(cmd, verbose):
         print(r.stderr, file=sys.stderr)
 
 
+PYFAST_SRC = os.path.join(CSRC, "ivc_pyfast.c")
+
+
+def pyfast_path() -> str:
+    import sysconfig
+    return os.path.join(HERE, "_lib", "_ivcfast" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_pyfast(verbose: bool = False) -> str:
+    """The CPython/NumPy accelerator of the per-block calls (ivc_pyfast.c): gcc, host only."""
+    import sysconfig
+    import numpy as np
+    out = pyfast_path()
+    if os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(PYFAST_SRC),
+                                                            os.path.getmtime(__file__)):
+        return out
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        raise RuntimeError("gcc not found (needed for the per-block call accelerator)")
+    tmp = out + ".tmp"
+    cmd = [cc, "-O2", "-shared", "-fPIC", "-Wall", "-I" + sysconfig.get_paths()["include"],
+           "-I" + np.get_include(), "-o", tmp, PYFAST_SRC]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"gcc failed ({r.returncode}):\n{r.stdout}\n{r.stderr}")
+    os.replace(tmp, out)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile each translation unit to an object (in parallel, under ivclab_amd/_lib/obj),
     then link the shared library."""
+    build_pyfast(verbose)
     if not force and up_to_date():
         return OUT
     from concurrent.futures import ThreadPoolExecutor

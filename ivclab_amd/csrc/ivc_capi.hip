@@ -172,6 +172,9 @@ struct DevCtx {
   int tiny_state = 0;                       // 0 untried, 1 ready, -1 unavailable
   uint32_t tiny_seq = 0;                    // last completion value written behind a tiny call
   uint32_t* tiny_count = nullptr;           // finished workgroups of the running tiny call
+  double* tiny_tab = nullptr;               // device copy of the last quantiser table of a tiny call
+  QTab tiny_tab_host;                       // its values
+  bool tiny_tab_valid = false;
   void* slot[kSlots] = {};
   size_t cap[kSlots] = {};
   void* pin[kPinSlots] = {};
@@ -208,6 +211,29 @@ bool tiny_ready(DevCtx* c) {
     (void)hipGetLastError();
   }
   return c->tiny_state == 1;
+}
+
+// The device copy of a tiny quantise / dequantise call's table (the per-block loops pass the
+// same table every call): compared by value, copied (synchronously: rare) when it changes;
+// nullptr when no copy can be made (the table then travels in the arguments).
+const double* tiny_table(DevCtx* c, const QTab& t) {
+  if (!c->tiny_tab && hipMalloc((void**)&c->tiny_tab, sizeof(QTab)) != hipSuccess) {
+    c->tiny_tab = nullptr;
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (!c->tiny_tab_valid || memcmp(c->tiny_tab_host.q, t.q, sizeof(QTab)) != 0) {
+    c->tiny_tab_valid = false;
+    // stream-ordered behind any earlier tiny call that still reads the old copy
+    if (hipMemcpyAsync(c->tiny_tab, t.q, sizeof(QTab), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    c->tiny_tab_host = t;
+    c->tiny_tab_valid = true;
+  }
+  return c->tiny_tab;
 }
 
 bool pinned_ready(DevCtx* c) {
@@ -729,7 +755,8 @@ int ivc_quantize(const void* src, int src_dtype, int64_t nblk, int C, const doub
   TRY(st.open());
   const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
   if (st.tiny(src, ib, dst, ob, "quantize", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
-        return launch_quantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s, d);
+        return launch_quantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s, d,
+                               tiny_table(st.ctx, t));
       }))
     return st.status;
   if (st.pipelined(src, (size_t)C * 64 * dtype_size(src_dtype), dst, 192 * 4, nblk, "quantize",
@@ -766,7 +793,8 @@ int ivc_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const do
   TRY(st.open());
   const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
   if (st.tiny(src, ib, dst, ob, "dequantize", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
-        return launch_dequantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s, d);
+        return launch_dequantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s, d,
+                                 tiny_table(st.ctx, t));
       }))
     return st.status;
   if (st.pipelined(src, (size_t)C * 64 * dtype_size(src_dtype), dst, 192 * 4, nblk, "dequantize",

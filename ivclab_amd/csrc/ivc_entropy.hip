@@ -416,6 +416,9 @@ __device__ __forceinline__ zv4 zw_load(const int32_t* src, int64_t nblk, int64_t
 #ifndef IVC_ZC
 #define IVC_ZC 1
 #endif
+#ifndef IVC_SLOT5
+#define IVC_SLOT5 1   // emission slots: 4 mbcnt + a shift-add (0: 6 mbcnt)
+#endif
 #ifndef IVC_ZC_NT
 #define IVC_ZC_NT 1
 #endif
@@ -701,12 +704,20 @@ __global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
       const bool rs = __builtin_amdgcn_inverse_ballot_w64(st);
       const int cnt = __builtin_popcountll(m) + 2 * __builtin_popcountll(st) + 1;
       // the lane's slot, fill included (mbcnt accumulates: m's bits below the lane, st's twice)
+#if IVC_SLOT5
+      uint32_t slot = __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)fill);
+      slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), slot);
+      uint32_t s2 = __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u);
+      s2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), s2);
+      slot += 2 * s2;
+#else
       uint32_t slot = __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)fill);
       slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), slot);
       slot = __builtin_amdgcn_mbcnt_lo((uint32_t)st, slot);
       slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), slot);
       slot = __builtin_amdgcn_mbcnt_lo((uint32_t)st, slot);
       slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), slot);
+#endif
       const bool w1 = nz || pnz;
       const int32_t v1 = nz || hl ? x : eob;
       // only the lanes with something to write touch LDS (exec-masked, so the idle lanes' words

@@ -120,11 +120,13 @@ hipError_t launch_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst
                          int inverse, int norm, hipStream_t s, const TinyDone* done = nullptr);
 hipError_t launch_dct8x8_image(const void* img, int src_dtype, int64_t rows, int64_t W, int64_t C,
                                void* dst, int dst_dtype, int inverse, int norm, hipStream_t s);
+// dtab (tiny calls only): a device copy of t the kernel reads instead of the argument copy
 hipError_t launch_quantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
-                           int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done = nullptr);
+                           int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done = nullptr,
+                           const double* dtab = nullptr);
 hipError_t launch_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
                              int calc_dtype, int32_t* dst, hipStream_t s,
-                             const TinyDone* done = nullptr);
+                             const TinyDone* done = nullptr, const double* dtab = nullptr);
 hipError_t launch_zigzag(const void* src, int64_t nrow, int64_t stride, int esize, int inverse,
                          void* dst, hipStream_t s, const TinyDone* done = nullptr);
 // returns hipErrorInvalidValue for an unsupported dtype / C combination

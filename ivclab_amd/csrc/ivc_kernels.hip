@@ -285,11 +285,24 @@ hipError_t launch_dct8x8_image(const void* img, int src_dtype, int64_t rows, int
 // Quantise / dequantise (patchquant.py:44-78).  Element-wise over the [blk][3][64] output,
 // 4 outputs (one 16-byte store) per thread; C = 1 inputs broadcast over the 3 planes.
 // ======================================================================================
-template <typename TI, typename D, typename TD>
+// The quantiser table: by value in the kernel arguments, or (a tiny call) a device copy the
+// C-ABI keeps of the last table used, so the arguments stay small (each 512 B of arguments
+// costs ~0.15 us of launch)
+template <bool TP> struct TabArg {
+  QTab t;
+  __device__ const double* q() const { return t.q; }
+};
+template <> struct TabArg<true> {
+  const double* p;
+  __device__ const double* q() const { return p; }
+};
+
+template <typename TI, typename D, typename TD, bool TP = false>
 __global__ __launch_bounds__(256) void quantize_kernel(const TI* __restrict__ src, int64_t nblk,
-                                                       int C, QTab t, int32_t* __restrict__ dst,
-                                                       TD done) {
+                                                       int C, TabArg<TP> tab,
+                                                       int32_t* __restrict__ dst, TD done) {
   src = tiny_src(src, done);
+  const double* tq = tab.q();
   const int64_t total = nblk * 48;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -299,17 +312,18 @@ __global__ __launch_bounds__(256) void quantize_kernel(const TI* __restrict__ sr
     int v[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      v[e] = np_to_i32<D>(rint_t<D>((D)sp[e] / (D)t.q[p * 64 + j + e]));
+      v[e] = np_to_i32<D>(rint_t<D>((D)sp[e] / (D)tq[p * 64 + j + e]));
     *reinterpret_cast<int4*>(dst + g * 4) = make_int4(v[0], v[1], v[2], v[3]);
   }
   tiny_done(done);
 }
 
-template <typename TI, typename D, typename TD>
+template <typename TI, typename D, typename TD, bool TP = false>
 __global__ __launch_bounds__(256) void dequantize_kernel(const TI* __restrict__ src,
-                                                         int64_t nblk, int C, QTab t,
+                                                         int64_t nblk, int C, TabArg<TP> tab,
                                                          int32_t* __restrict__ dst, TD done) {
   src = tiny_src(src, done);
+  const double* tq = tab.q();
   const int64_t total = nblk * 48;
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
        g += (int64_t)gridDim.x * blockDim.x) {
@@ -318,7 +332,7 @@ __global__ __launch_bounds__(256) void dequantize_kernel(const TI* __restrict__ 
     const TI* sp = src + (blk * C + (C == 1 ? 0 : p)) * 64 + j;
     int v[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = np_to_i32<D>((D)sp[e] * (D)t.q[p * 64 + j + e]);
+    for (int e = 0; e < 4; ++e) v[e] = np_to_i32<D>((D)sp[e] * (D)tq[p * 64 + j + e]);
     *reinterpret_cast<int4*>(dst + g * 4) = make_int4(v[0], v[1], v[2], v[3]);
   }
   tiny_done(done);
@@ -327,50 +341,56 @@ __global__ __launch_bounds__(256) void dequantize_kernel(const TI* __restrict__ 
 template <bool DEQ>
 static hipError_t launch_quant_common(const void* src, int src_dtype, int64_t nblk, int C,
                                       const QTab& t, int calc_dtype, int32_t* dst,
-                                      hipStream_t s, const TinyDone* done) {
+                                      hipStream_t s, const TinyDone* done, const double* dtab) {
   if (nblk <= 0) return hipSuccess;
   if (C != 1 && C != 3) return hipErrorInvalidValue;
   unsigned grid = grid_for(nblk * 48, 256, 16);
-  // one (3, 8, 8) stack (a tiny host call): one wave, not four
+  // one (3, 8, 8) stack (a tiny call): one wave, not four
   const unsigned nt = nblk * 48 <= 64 ? 64 : 256;
-  if (calc_dtype == IVC_F32) {
-    // float32 arithmetic only arises for float32 or <= 16-bit integer inputs
-    if (dtype_size(src_dtype) > 2 && src_dtype != IVC_F32) return hipErrorInvalidValue;
-    return with_tiny(done, [&](auto dn) -> hipError_t {
-      using TD = decltype(dn);
+  if (calc_dtype != IVC_F32 && calc_dtype != IVC_F64) return hipErrorInvalidValue;
+  // float32 arithmetic only arises for float32 or <= 16-bit integer inputs
+  if (calc_dtype == IVC_F32 && dtype_size(src_dtype) > 2 && src_dtype != IVC_F32)
+    return hipErrorInvalidValue;
+  return with_tiny(done, [&](auto dn) -> hipError_t {
+    using TD = decltype(dn);
+    auto go = [&](auto tabc) {
+      constexpr bool TP = decltype(tabc)::value;
+      TabArg<TP> tab;
+      if constexpr (TP) tab.p = dtab; else tab.t = t;
       IVC_DISPATCH_ALL(src_dtype, {
-        if constexpr (sizeof(TI) <= 2 || std::is_same<TI, float>::value) {
+        if (calc_dtype == IVC_F32) {
+          if constexpr (sizeof(TI) <= 2 || std::is_same<TI, float>::value) {
+            if (DEQ)
+              dequantize_kernel<TI, float, TD, TP><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, tab, dst, dn);
+            else
+              quantize_kernel<TI, float, TD, TP><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, tab, dst, dn);
+          }
+        } else {
           if (DEQ)
-            dequantize_kernel<TI, float, TD><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
+            dequantize_kernel<TI, double, TD, TP><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, tab, dst, dn);
           else
-            quantize_kernel<TI, float, TD><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
+            quantize_kernel<TI, double, TD, TP><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, tab, dst, dn);
         }
       });
       return hipGetLastError();
-    });
-  }
-  if (calc_dtype == IVC_F64) {
-    return with_tiny(done, [&](auto dn) -> hipError_t {
-      using TD = decltype(dn);
-      IVC_DISPATCH_ALL(src_dtype, {
-        if (DEQ)
-          dequantize_kernel<TI, double, TD><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
-        else
-          quantize_kernel<TI, double, TD><<<grid, nt, 0, s>>>((const TI*)src, nblk, C, t, dst, dn);
-      });
-      return hipGetLastError();
-    });
-  }
-  return hipErrorInvalidValue;
+    };
+    // the device table only behind a tiny call's argument-borne input
+    if constexpr (IsTinyIn<TD>::value) {
+      if (dtab) return go(std::true_type{});
+    }
+    return go(std::false_type{});
+  });
 }
 
 hipError_t launch_quantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
-                           int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done) {
-  return launch_quant_common<false>(src, src_dtype, nblk, C, t, calc_dtype, dst, s, done);
+                           int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done,
+                           const double* dtab) {
+  return launch_quant_common<false>(src, src_dtype, nblk, C, t, calc_dtype, dst, s, done, dtab);
 }
 hipError_t launch_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const QTab& t,
-                             int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done) {
-  return launch_quant_common<true>(src, src_dtype, nblk, C, t, calc_dtype, dst, s, done);
+                             int calc_dtype, int32_t* dst, hipStream_t s, const TinyDone* done,
+                             const double* dtab) {
+  return launch_quant_common<true>(src, src_dtype, nblk, C, t, calc_dtype, dst, s, done, dtab);
 }
 
 // ======================================================================================
@@ -513,6 +533,9 @@ struct FusedArgs {
 #endif
 #ifndef IVC_C3_SPLIT
 #define IVC_C3_SPLIT 1         // C = 3 coefficients, small launches: one wave per (group, plane)
+#endif
+#ifndef IVC_SLOT5
+#define IVC_SLOT5 1            // emission slots: 4 mbcnt + a shift-add (tools/ab A/B: 0 = 6 mbcnt)
 #endif
 #ifndef IVC_COUNT_PREFETCH
 #define IVC_COUNT_PREFETCH 1   // the symbol count pass: one tile ahead (2: 7.05 vs 6.96 ms for
@@ -1056,12 +1079,21 @@ __device__ __forceinline__ uint32_t zh_bin(const FusedArgs& a, int32_t v, int la
 // check (one basic block for the group).  Same slots and values as the general path below.
 // a lane's emission slot: base + (bits of m below the lane) + 2 (bits of st below the lane)
 __device__ __forceinline__ int emit_slot(uint64_t m, uint64_t st, int base) {
+#if IVC_SLOT5
+  // four mbcnt and one shift-add (st's count doubled) instead of six mbcnt
+  uint32_t t = __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)base);
+  t = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), t);
+  uint32_t u = __builtin_amdgcn_mbcnt_lo((uint32_t)st, 0u);
+  u = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), u);
+  return (int)(t + 2 * u);
+#else
   uint32_t t = __builtin_amdgcn_mbcnt_lo((uint32_t)m, (uint32_t)base);
   t = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), t);
   t = __builtin_amdgcn_mbcnt_lo((uint32_t)st, t);
   t = __builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), t);
   t = __builtin_amdgcn_mbcnt_lo((uint32_t)st, t);
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(st >> 32), t);
+#endif
 }
 template <int C, bool DUP, bool HIST>
 __device__ __forceinline__ void zr_group_emit_fit(const FusedArgs& a, int32_t* os, int64_t gbase,

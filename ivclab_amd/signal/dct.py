@@ -31,9 +31,18 @@ _F32 = np.dtype(np.float32)
 
 def dct2d(a, norm="ortho", inverse=False) -> np.ndarray:
     """dct (or idct) along axis -1 then axis -2 of every trailing 8x8 block of `a`."""
-    # fast path for small C-contiguous arrays of a supported dtype (the reference's per-block
-    # loops call this once per (8, 8) block: the general checks below cost more than the GPU
-    # round trip's host side)
+    # fast path for small arrays of a supported dtype (the reference's per-block loops call
+    # this once per (8, 8) block: the general checks below cost more than the GPU round trip's
+    # host side): C-contiguous ones in one C step (ivc_pyfast.c), others through ctypes
+    if type(a) is np.ndarray and a.size <= 4096:
+        F = N.fast()
+        nc = N.NORM_CODE.get(norm)
+        if F is not None and nc is not None:
+            r = F.dct8x8(a, nc, 1 if inverse else 0)
+            if r is not None:
+                if type(r) is int:
+                    N.check(r, "DiscreteCosineTransform")
+                return r
     if type(a) is np.ndarray and a.shape[-2:] == (8, 8) and 0 < a.size <= 4096:
         code = N.DTYPE_CODE.get(a.dtype)
         nc = N.NORM_CODE.get(norm)
