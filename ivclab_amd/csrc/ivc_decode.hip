@@ -50,6 +50,9 @@ constexpr int DX_WAVE = 8 * 72;  // doubles per wave: transpose image [b][k pitc
 #ifndef IVC_DEC_STORE_AUX
 #define IVC_DEC_STORE_AUX 2      // nt: streamed output
 #endif
+#ifndef IVC_DEC_PAD_ZERO
+#define IVC_DEC_PAD_ZERO 1       // sym_image_kernel: no per-symbol bound test (see the parse)
+#endif
 // ablation builds only (tools/ab), bits: 1 = the image stores skipped (behind a runtime test the
 // compiler cannot fold), 2 = sym_image_kernel's parse skipped (the staging stays zero)
 #ifndef IVC_DEC_ABLATE
@@ -389,7 +392,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int prv = e ? v[e - 1] : pvs, nx = e < 3 ? v[e + 1] : nxs;
-          const bool valid = i0 + e < rlen;
+          // Past the group's last symbol (its last EOB) the staging holds zeros (the buffer
+          // range ends there): the first is a value slot holding 0, which adds one coefficient
+          // past the last block-plane (no write, no EOB, no failure), every later one a
+          // run-length slot — so the tail needs no validity test
+          const bool valid = IVC_DEC_PAD_ZERO || i0 + e < rlen;
           const bool rl = prv == 0;                    // a run-length slot
           eobf[e] = valid && !rl && v[e] == z.eob;
           isval[e] = valid && !rl && !eobf[e];
