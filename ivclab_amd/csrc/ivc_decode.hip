@@ -397,12 +397,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
           // past the last block-plane (no write, no EOB, no failure), every later one a
           // run-length slot — so the tail needs no validity test
           const bool valid = IVC_DEC_PAD_ZERO || i0 + e < rlen;
-          const bool rl = prv == 0;                    // a run-length slot
-          eobf[e] = valid && !rl && v[e] == z.eob;
-          isval[e] = valid && !rl && !eobf[e];
+          const bool slot = valid && prv != 0;         // not a run-length slot
+          const bool ise = v[e] == z.eob;
+          eobf[e] = slot && ise;
+          isval[e] = slot && !ise;
           const int run = nx < 1 ? 1 : (nx > 127 ? 127 : nx);
-          const int cc = isval[e] ? (v[e] == 0 ? run : 1) : 0;
-          pk[e] = (eobf[e] ? (1 << 16) : 0) | cc;
+          // (EOB flag << 16) | coefficient count, as one select chain: EOB, else a value's
+          // count (the run length for a 0), else (a run-length slot) nothing
+          const int f = ise ? (1 << 16) : (v[e] == 0 ? run : 1);
+          pk[e] = slot ? f : 0;
           lt += pk[e];
         }
         const int incl = dec_wave_incl_sum(lt);
@@ -424,9 +427,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
         for (int e = 0; e < 4; ++e) {
           const bool bpok = bp[e] < nbp;
           const int off = pex[e] - bs[e];             // offset inside the block-plane
-          const bool nzv = isval[e] && v[e] != 0;
-          const bool wr = nzv && off < 64 && bpok && v[e] == (int)(int16_t)v[e];
-          bad |= (nzv && !wr) || (eobf[e] && (off > 64 || !bpok));
+          // (non-short-circuit & and |: lane masks combined by the scalar unit, no branches)
+          const bool nzv = isval[e] & (v[e] != 0);
+          const bool wr = nzv & (off < 64) & bpok & (v[e] == (int)(int16_t)v[e]);
+          bad |= (nzv & !wr) | (eobf[e] & ((off > 64) | !bpok));
           if (wr) qs[__umul24(bp[e], SYM_QP) + off] = (int16_t)v[e];
         }
         const int tot = __builtin_amdgcn_readlane(incl, 63);
