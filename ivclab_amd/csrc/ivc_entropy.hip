@@ -902,6 +902,12 @@ hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int
 #ifndef IVC_ZR_CHUNKS
 #define IVC_ZR_CHUNKS 32
 #endif
+#ifndef IVC_ZR_COUNT_WGCU
+#define IVC_ZR_COUNT_WGCU 8     // the pipelined call's workgroups per CU: count pass
+#endif
+#ifndef IVC_ZR_EMIT_WGCU
+#define IVC_ZR_EMIT_WGCU 6      // and emission
+#endif
 #ifndef IVC_ZR_MIN_CHUNK
 #define IVC_ZR_MIN_CHUNK 98304
 #endif
@@ -940,7 +946,7 @@ hipError_t launch_zerorun_encode(const int32_t* src, int64_t nblk, int stride, i
     const int64_t g0 = std::min<int64_t>((int64_t)j * per, ng), g1 = std::min<int64_t>(g0 + per, ng);
     if (g1 <= g0) break;
     const int64_t len = g1 - g0;
-    zw_count_kernel<true><<<zw_grid((len * ZW_BLK + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, 8), 256, 0, s>>>(
+    zw_count_kernel<true><<<zw_grid((len * ZW_BLK + IVC_ZW_COUNT_GROUPS - 1) / IVC_ZW_COUNT_GROUPS, IVC_ZR_COUNT_WGCU), 256, 0, s>>>(
         src, nblk, z.counts, z.zc, g0, g1);
     // the chunk's scan on the second stream ahead of its emission, so the caller's stream runs
     // the count passes back to back (small scan kernels there waited behind the high-priority
@@ -952,7 +958,7 @@ hipError_t launch_zerorun_encode(const int32_t* src, int64_t nblk, int stride, i
                                                   g1 == ng ? off + nblk : nullptr},
                              z.agg, P.aux);
     if (e != hipSuccess) return e;
-    zc_emit_kernel<<<zw_grid(len * ZW_BLK, 6), 256, 0, P.aux>>>(nblk, eob, z.goff, z.zc.c8, z.zc.c16,
+    zc_emit_kernel<<<zw_grid(len * ZW_BLK, IVC_ZR_EMIT_WGCU), 256, 0, P.aux>>>(nblk, eob, z.goff, z.zc.c8, z.zc.c16,
                                                               z.zc.flag, z.zc.ctl + 1, off, out,
                                                               capacity, g0, g1);
     if ((e = hipGetLastError()) != hipSuccess) return e;

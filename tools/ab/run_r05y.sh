@@ -1,0 +1,9 @@
+#!/bin/bash
+# r05y: zero-run encoder pipeline grid knobs (count / emission workgroups per CU, groups per
+# count wave)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python tools/ab/ab_symbols.py ab/zrb.so ab/zrg2.so ab/zrg1.so ab/zrg2c12.so ab/zrg2c16.so --rounds 4 --legs zerorun_encode > gpurun_out/r05y_ab_zr.log 2>&1 || { tail -20 gpurun_out/r05y_ab_zr.log; exit 1; }
+cat gpurun_out/r05y_ab_zr.log
