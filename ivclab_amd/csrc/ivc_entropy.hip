@@ -437,7 +437,9 @@ struct ZcScratch {
 // not nblk); the emit pass derives each block's offset from its group's offset and the
 // counts of the group's earlier blocks, and writes offsets[blk] itself.
 #ifndef IVC_ZW_COUNT_GROUPS
-#define IVC_ZW_COUNT_GROUPS 4   // 16-block groups per wave-iteration of the count pass (4: -2%)
+#define IVC_ZW_COUNT_GROUPS 2   // 16-block groups per wave-iteration of the count pass (r05,
+                                // pipelined call: 2 against 4, 10.33 -> 10.16 ms; 1: 10.33 ms,
+                                // profiles/r05y_ab_zerorun_count_groups.log)
 #endif
 // groups [g_begin, g_end) (g_end < 0: all)
 template <bool EXPORT>
