@@ -908,8 +908,9 @@ hipError_t launch_zerorun_emit(const int32_t* src, int64_t nblk, int stride, int
 #define IVC_ZR_COUNT_WGCU 8     // the pipelined call's workgroups per CU: count pass
 #endif
 #ifndef IVC_ZR_EMIT_WGCU
-#define IVC_ZR_EMIT_WGCU 6      // and emission
-#endif
+#define IVC_ZR_EMIT_WGCU 5      // and emission (6: 10.41 / 10.15 ms against 10.18 / 9.86 ms for 5 on
+#endif                          // two boxes; several other pairs fall to 13-15 ms: the two
+                                // streams' grids then serialise — profiles/r05x/z/aa_ab_zerorun_*)
 #ifndef IVC_ZR_MIN_CHUNK
 #define IVC_ZR_MIN_CHUNK 98304
 #endif
