@@ -1484,6 +1484,11 @@ __global__ void s2i_rejected_verdict(const int* ok, int64_t* err) {
 #ifndef IVC_S2I_CHUNKS
 #define IVC_S2I_CHUNKS 32
 #endif
+#ifndef IVC_S2I_COUNT_WGCU
+#define IVC_S2I_COUNT_WGCU 2     // the pipelined call's EOB pass: workgroups per CU (2: 14.89,
+                                 // 4: 14.93, 6: 17.47 (the streams serialise), 8: 15.08 ms,
+                                 // profiles/r05ab_ab_decode_count_grid.log)
+#endif
 #ifndef IVC_S2I_MIN_CHUNK
 #define IVC_S2I_MIN_CHUNK 16384
 #endif
@@ -1523,7 +1528,7 @@ static hipError_t s2i_pipelined(const int32_t* sym, int64_t n, int32_t eob, int6
     const int64_t a = tile0(j), b = tile0(j + 1);
     if (b > a) {
       const int64_t len = b - a;
-      const unsigned grid = (unsigned)(len < 256 * 8 ? len : 256 * 8);
+      const unsigned grid = (unsigned)(len < 256 * IVC_S2I_COUNT_WGCU ? len : 256 * IVC_S2I_COUNT_WGCU);
       zf_count_kernel<<<grid, 256, 0, s>>>(sym, n, eob, z.tile_eobs, z.flags, z.eobmask, a, b);
       e = device_scan<int64_t>(len, CountGen{z.tile_eobs + a}, SumI64{},
                                OffsetCarrySink{z.tile_first + a, len, z.tile_first + a}, z.fagg, s);
