@@ -241,7 +241,7 @@ __global__ __launch_bounds__(256) void intra_decode_kernel(DecArgs a, QTab t) {
   for (int i = tid; i < 192; i += 256) tq[i] = t.q[i];
   uint32_t pos[2];
   dec_gather_pos<ZZ>(r, pos);
-  __syncthreads();   // the table only: the loop never synchronises across waves
+  lds_barrier();   // the table only: the loop never synchronises across waves
 
   int32_t* qs = qs_all + wave * QS;
   double* xs = xs_all + wave * DX_WAVE;
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   for (int i = tid; i < 192; i += 256) tq[i] = t.q[i];
   uint32_t pos[2];
   dec_gather_pos<true>(r, pos);
-  __syncthreads();   // the table only
+  lds_barrier();   // the table only
 
   int16_t* qs = qs_all + wave * QS;
   int* bps = bps_all + wave * 32;

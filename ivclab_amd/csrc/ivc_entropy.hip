@@ -103,11 +103,11 @@ __device__ T wg_excl_scan(T v, Op op, T* lds4, T& total) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const T incl = wave_incl_scan(v, op);
   if (lane == 63) lds4[wave] = incl;
-  __syncthreads();
+  lds_barrier();
   T before = Op::identity();
   for (int w = 0; w < wave; ++w) before = op(before, lds4[w]);
   total = op(op(op(lds4[0], lds4[1]), lds4[2]), lds4[3]);
-  __syncthreads();
+  lds_barrier();
   const T excl_in_wave = shfl_up_t(incl, 1);
   return op(before, lane == 0 ? Op::identity() : excl_in_wave);
 }
@@ -1257,7 +1257,7 @@ __global__ __launch_bounds__(256) void zf_expand_kernel(const int32_t* __restric
       }
     }
     if (tid == 0) last_halo = T0 == 0 ? -1 : -2;
-    __syncthreads();
+    lds_barrier();
     auto is_eob = [&](int j) {               // j relative to h0, symbol h0 + j
       return sh[j] == eob && (h0 + j == 0 || sh[j - 1] != 0);
     };
@@ -1270,7 +1270,7 @@ __global__ __launch_bounds__(256) void zf_expand_kernel(const int32_t* __restric
     for (int e = 0; e < PER; ++e) c += (j0 + e < len && is_eob(j0 + e)) ? 1 : 0;
     const int incl = zf_wave_incl_sum(c);
     if (lane == 63) cnt_w[wave] = incl;
-    __syncthreads();
+    lds_barrier();
     int before = 0;
     for (int w = 0; w < wave; ++w) before += cnt_w[w];
     const int m = cnt_w[0] + cnt_w[1] + cnt_w[2] + cnt_w[3];
@@ -1278,7 +1278,7 @@ __global__ __launch_bounds__(256) void zf_expand_kernel(const int32_t* __restric
 #pragma unroll
     for (int e = 0; e < PER; ++e)
       if (j0 + e < len && is_eob(j0 + e)) epos[o++] = j0 + e;
-    __syncthreads();
+    lds_barrier();
     if (m > 0 && last_halo == -2 && tid == 0) atomicOr(fail, 1);   // a block longer than the halo
     const int64_t first = tile_first[t];
     for (int k = wave; k < m; k += 4) {
@@ -1322,7 +1322,7 @@ __global__ __launch_bounds__(256) void zf_expand_kernel(const int32_t* __restric
       }
       __builtin_amdgcn_wave_barrier();
     }
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -1684,7 +1684,7 @@ __global__ __launch_bounds__(256) void edge_histogram_kernel(const double* __res
   if (LDS) {
     for (int i = threadIdx.x; i < nedges; i += 256) e_s[i] = edges_g[i];
     for (int i = threadIdx.x; i < nb; i += 256) c_s[i] = 0;
-    __syncthreads();
+    lds_barrier();
     edges = e_s;
   }
   const double lo = edges[0], hi = edges[nb];
@@ -1706,7 +1706,7 @@ __global__ __launch_bounds__(256) void edge_histogram_kernel(const double* __res
     else atomicAdd(&counts[b], 1ull);
   }
   if (LDS) {
-    __syncthreads();
+    lds_barrier();
     for (int j = threadIdx.x; j < nb; j += 256)
       if (c_s[j]) atomicAdd(&counts[j], (unsigned long long)c_s[j]);
   }

@@ -10,6 +10,17 @@
 
 namespace ivc {
 
+// The workgroup barrier of every kernel: the wave's own LDS operations drained, then the
+// barrier.  hipcc (ROCm 7.2) leaves out the lgkmcnt(0) wait at some barriers (loop headers
+// reached with LDS writes still in flight from the back edge), and on gfx950 another wave then
+// occasionally reads the LDS word as it was before the write: me_mfma16x2_kernel's cross-wave
+// merge picked up a stale per-wave result in 12 of 300 cfg5 steps, 0 of 450 with the wait
+// (tools/race_probe.py, profiles/r05ai_race_probe.log).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 // the per-device second stream of the pipelined calls (ivc_entropy.hip)
 constexpr int PIPE_EVENTS = 66;
 struct PipeCtx {
@@ -100,7 +111,7 @@ template <typename TD>
 __device__ __forceinline__ void tiny_done(const TD& d) {
   if (d.flag == nullptr) return;                      // uniform
   __threadfence_system();                             // this thread's writes, system scope
-  __syncthreads();
+  lds_barrier();
   if (threadIdx.x == 0) {
     if (gridDim.x == 1) {                             // the common tiny call: no counter
       __hip_atomic_store(d.flag, d.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -138,21 +138,21 @@ __global__ __launch_bounds__(256) void dct8x8_kernel(const TI* __restrict__ src,
     if constexpr (INV) dct3_line<T>(x, fct, ortho != 0); else dct2_line<T>(x, fct, ortho != 0);
 #pragma unroll
     for (int k = 0; k < 8; ++k) xs[u * 72 + r * 9 + k] = x[k];
-    __syncthreads();
+    lds_barrier();
 #pragma unroll
     for (int i = 0; i < 8; ++i) x[i] = xs[u * 72 + i * 9 + r];
-    __syncthreads();
+    lds_barrier();
     if constexpr (INV) dct3_line<T>(x, fct, ortho != 0); else dct2_line<T>(x, fct, ortho != 0);
 #pragma unroll
     for (int i = 0; i < 8; ++i) xs[u * 64 + i * 8 + r] = x[i];
-    __syncthreads();
+    lds_barrier();
     const int64_t left = nunit - g * 32;
     const int nvalid = left < 32 ? (int)left : 32;
     constexpr int EPC = 16 / (int)sizeof(T);  // elements per 16-byte chunk
     T* out = dst + g * 32 * 64;
     for (int e = tid * EPC; e < nvalid * 64; e += 256 * EPC)
       *reinterpret_cast<uint4*>(out + e) = *reinterpret_cast<const uint4*>(xs + e);
-    __syncthreads();
+    lds_barrier();
   }
   tiny_done(done);
 }
@@ -536,6 +536,12 @@ struct FusedArgs {
 #endif
 #ifndef IVC_SLOT5
 #define IVC_SLOT5 1            // emission slots: 4 mbcnt + a shift-add (tools/ab A/B: 0 = 6 mbcnt)
+#endif
+#ifndef IVC_SYM_COUNT_FRAC
+#define IVC_SYM_COUNT_FRAC 8   // eighths of the resident grid for the count pass (8: all of it)
+#endif
+#ifndef IVC_SYM_EMIT_FRAC
+#define IVC_SYM_EMIT_FRAC 8    // and for the pipelined emitter
 #endif
 #ifndef IVC_COUNT_PREFETCH
 #define IVC_COUNT_PREFETCH 1   // the symbol count pass: one tile ahead (2: 7.05 vs 6.96 ms for
@@ -1459,7 +1465,7 @@ void fused_encode_kernel(FusedArgs a, QTab t) {
     for (int i = tid; i < ZH_LDS; i += 256) zh[i] = 0;
     hacc.bins = zh;
   }
-  __syncthreads();  // tables only; the loop below never synchronises across waves (but the
+  lds_barrier();  // tables only; the loop below never synchronises across waves (but the
                     // symbol histogram's bins are flushed after a barrier at the end)
 
   unsigned char* mine = lds + wave * L::BYTES;
@@ -1638,7 +1644,7 @@ void fused_encode_kernel(FusedArgs a, QTab t) {
     }
   }
   if constexpr (OUTM == OUT_SYMH || OUTM == OUT_COEFH) {
-    __syncthreads();
+    lds_barrier();
     zh_flush(a, zh, tid);
   }
 }
@@ -2220,7 +2226,7 @@ __global__ __launch_bounds__(256) void sym_emit_kernel(FusedArgs a, int64_t ngro
   if constexpr (HIST) {
     for (int i = tid; i < ZH_LDS; i += 256) zh[i] = 0;
     hacc.bins = zh;
-    __syncthreads();
+    lds_barrier();
   }
   int32_t* os = win + wave * ZR_WIN;
   const int64_t nw = (int64_t)gridDim.x * 4;
@@ -2283,7 +2289,7 @@ __global__ __launch_bounds__(256) void sym_emit_kernel(FusedArgs a, int64_t ngro
     cur = nxt;
   }
   if constexpr (HIST) {
-    __syncthreads();
+    lds_barrier();
     zh_flush(a, zh, tid);
   }
 }
@@ -2295,7 +2301,9 @@ static void launch_fused_zr(const FusedArgs& a_in, const QTab& t, hipStream_t s)
   a.tpr = (a.w + 8 * NG - 1) / (8 * NG);
   const int64_t nlt = (int64_t)a.nframes * a.h * a.tpr;
   auto k = fused_encode_kernel<TI, double, double, C, true, true, SRC_IMAGE, CM, NG, DUP, OUTM>;
-  k<<<resident_grid(k, (nlt + 3) / 4), 256, 0, s>>>(a, t);
+  unsigned grid = resident_grid(k, (nlt + 3) / 4);
+  if (OUTM == OUT_COUNT && IVC_SYM_COUNT_FRAC < 8) grid = grid * IVC_SYM_COUNT_FRAC / 8 + 1;
+  k<<<grid, 256, 0, s>>>(a, t);
 }
 
 // The count pass and the emitter pipelined over K chunks of whole frames (like the zero-run
@@ -2388,7 +2396,9 @@ static hipError_t intra_symbols_pipelined(const FusedArgs& a, int64_t gpf, int K
     if ((e = hipStreamWaitEvent(P.aux, P.ev[j], 0)) != hipSuccess) return e;
     if ((e = launch_exclusive_scan_i32_carry(ac.zr_counts, len, agg, off + g0, P.aux)) != hipSuccess)
       return e;
-    k<<<resident_grid(k, (len + 3) / 4), 256, 0, P.aux>>>(ac, len, ac.zr_counts, ac.zr_off, ac.zr_cflag);
+    unsigned eg = resident_grid(k, (len + 3) / 4);
+    if (IVC_SYM_EMIT_FRAC < 8) eg = eg * IVC_SYM_EMIT_FRAC / 8 + 1;
+    k<<<eg, 256, 0, P.aux>>>(ac, len, ac.zr_counts, ac.zr_off, ac.zr_cflag);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   join.armed = false;
@@ -2570,7 +2580,7 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
   const int tid = threadIdx.x;
   if (use_lds) {
     for (int i = tid; i < nbins; i += 256) bins[i] = 0;
-    __syncthreads();
+    lds_barrier();
   }
   uint32_t hot[HIST_HOT_N];
 #pragma unroll
@@ -2656,7 +2666,7 @@ __global__ __launch_bounds__(256) void histogram_kernel(const S* __restrict__ sy
     }
   }
   if (use_lds) {
-    __syncthreads();
+    lds_barrier();
     for (int i2 = tid; i2 < nbins; i2 += 256)
       if (bins[i2]) atomicAdd(&hist[i2], (unsigned long long)bins[i2]);
   }

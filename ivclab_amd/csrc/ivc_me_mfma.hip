@@ -268,7 +268,10 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
     uint32_t f;
     int by, bx0;
     tile_xy(tile, f, by, bx0);
-    __syncthreads();                                   // the previous tile's LDS reads are done
+    // the previous tile's LDS reads are done and its search's red[] writes have landed (this
+    // barrier is the loop header: without lds_barrier's wait the merge below read stale
+    // entries, ivc_internal.h)
+    lds_barrier();
     if (have_prev) merge(pf, pby, pbx0);
     int ts = tid;
     asm volatile("" : "+v"(ts));
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
     {
       // window energies E[R][u] = B + 128 (-S2') (the header's form), two threads per
       // column u: threads 0..95 the offsets R < 20 from rows 0..26, threads 128..223 the
@@ -331,7 +334,7 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
     }
     const mf_v4i bop = mf_v4i{L.bop.x ^ (int)0x80808080u, L.bop.y ^ (int)0x80808080u,
                               L.bop.z ^ (int)0x80808080u, L.bop.w ^ (int)0x80808080u};
-    __syncthreads();
+    lds_barrier();
     load(tile + gridDim.x, L);                          // the next tile's inputs, in flight
     if (wave == 0) me2_search<0>(lds, red, wave, g, l16, bop);
     else if (wave == 3) me2_search<3>(lds, red, wave, g, l16, bop);
@@ -342,7 +345,7 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
     have_prev = true;
   }
   // the last tile's merge (every wave reaches this barrier: the loop bound is workgroup-uniform)
-  __syncthreads();
+  lds_barrier();
   if (have_prev) merge(pf, pby, pbx0);
 }
 

@@ -131,7 +131,7 @@ __global__ __launch_bounds__(256) void me_generic_kernel(const T* __restrict__ r
     const int y = 8 * by, x = 8 * bx;
     const int64_t fo = f * (int64_t)H * W;
     if (tid < 64) cb[tid] = cur[fo + (int64_t)(y + (tid >> 3)) * W + x + (tid & 7)];
-    __syncthreads();
+    lds_barrier();
     acc best = acc(0);
     int bidx = 0x7fffffff;
     for (int c = tid; c < nc; c += 256) {
@@ -144,7 +144,7 @@ __global__ __launch_bounds__(256) void me_generic_kernel(const T* __restrict__ r
     }
     sval[tid] = best;
     sidx[tid] = bidx;
-    __syncthreads();
+    lds_barrier();
     for (int off = 128; off > 0; off >>= 1) {
       if (tid < off) {
         const int ib = sidx[tid + off];
@@ -157,10 +157,10 @@ __global__ __launch_bounds__(256) void me_generic_kernel(const T* __restrict__ r
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
     }
     if (tid == 0) mv[blk] = sidx[0] == 0x7fffffff ? (int64_t)sr * n + sr : (int64_t)sidx[0];
-    __syncthreads();
+    lds_barrier();
   }
 }
 
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(FLT_WG, sizeof(T) == 8 ? 2 : 4) void me_flt_kernel(
       kmin[i] = ~(U)0;
       imin[i] = ~0u;
     }
-    __syncthreads();
+    lds_barrier();
     T best = T(0);
     int bidx = -1;
     const int rx = 8 * (bx0 + sb) + se - sr;
@@ -327,12 +327,12 @@ __global__ __launch_bounds__(FLT_WG, sizeof(T) == 8 ? 2 : 4) void me_flt_kernel(
       }
     }
     if (bidx >= 0) atomicMin(&kmin[sb], FltBits<T>::bits(best));
-    __syncthreads();
+    lds_barrier();
     if (bidx >= 0 && FltBits<T>::bits(best) == kmin[sb]) atomicMin(&imin[sb], (unsigned)bidx);
-    __syncthreads();
+    lds_barrier();
     if (tid < nb)
       mv[(f * h + by) * w + bx0 + tid] = imin[tid] == ~0u ? (int64_t)sr * n + sr : (int64_t)imin[tid];
-    __syncthreads();
+    lds_barrier();
   }
 }
 

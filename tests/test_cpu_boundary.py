@@ -209,3 +209,30 @@ def test_pmc_record_key_matches_bench():
     rec = json.load(open(os.path.join(root, "profiles", "pmc_intra_latest.json")))
     assert {"hbm_bytes_per_launch", "frames", "H", "W", "csrc_sha256"} <= set(rec)
     assert 0.99 < rec["hbm_bytes_per_launch"] / rec["algorithmic_bytes_per_launch"] < 1.05
+
+
+def test_device_barriers_drain_lds():
+    """Every workgroup barrier in the device sources goes through ivc::lds_barrier (an
+    lgkmcnt(0) wait, then the barrier): hipcc omits that wait at some loop-header barriers and
+    on gfx950 another wave can then read a stale LDS word (ivc_internal.h; the compiled-code
+    check is tools/check_barriers.py)."""
+    csrc = os.path.join(ROOT, "ivclab_amd", "csrc")
+    offenders = []
+    for name in sorted(os.listdir(csrc)):
+        if not name.endswith((".hip", ".h")):
+            continue
+        with open(os.path.join(csrc, name)) as f:
+            for n, line in enumerate(f, 1):
+                code = line.split("//")[0]
+                if re.search(r"__syncthreads\s*\(|__builtin_amdgcn_s_barrier\s*\(", code) and \
+                        "asm volatile(\"s_waitcnt lgkmcnt(0)\"" not in code:
+                    offenders.append(f"{name}:{n}")
+    # the one raw barrier is lds_barrier's own
+    assert offenders == ["ivc_internal.h:" + str(_lds_barrier_line(csrc))], offenders
+
+
+def _lds_barrier_line(csrc):
+    with open(os.path.join(csrc, "ivc_internal.h")) as f:
+        lines = f.read().split("\n")
+    start = next(i for i, l in enumerate(lines) if "void lds_barrier()" in l)
+    return next(i for i in range(start, start + 4) if "__syncthreads()" in lines[i]) + 1
