@@ -658,7 +658,11 @@ __global__ __launch_bounds__(256) void zc_emit_kernel(int64_t nblk, int32_t eob,
   auto fetch = [&](int64_t g, Pre& P) {
     P.base = goff[g];
     P.flag = gflag[g];
+#if IVC_ZC_NT
     P.w = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(c8 + (g * 64 + lane) * 16));
+#else
+    P.w = *reinterpret_cast<const i32x4*>(c8 + (g * 64 + lane) * 16);
+#endif
   };
   const int64_t g0 = g_begin + (int64_t)blockIdx.x * 4 + wave;
   Pre cur;

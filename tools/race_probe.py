@@ -4,7 +4,7 @@ and histogram bitwise with the first run's and with one unchunked, single-stream
 mismatch print where (pair, block row, block column) and in which tensor.  Diagnostic for an
 intermittent histogram mismatch (profiles/r05_race.md).
 
-  python tools/race_probe.py [--reps 12] [--frames 120] [--mode chunked|unchunked|noside]
+  python tools/race_probe.py [--reps 12] [--frames 120] [--mode chunked|unchunked|noside|intra]
 """
 import argparse
 import os
@@ -49,6 +49,61 @@ def ssd_report(seq, mv, mvr, sr, limit=6):
         print(f"  block ({p}, {by}, {bx}): got {out[0]}  want {out[1]}", flush=True)
 
 
+def intra(args, dev):
+    """cfg3 (256 x 4K luma): the pipelined pixels -> symbols call with its histogram, the
+    pipelined zero-run encode and the pipelined symbols -> image call, each run compared bit
+    for bit with the two-step stream / the first run's outputs"""
+    L = N.lib()
+    stream = torch.cuda.current_stream().cuda_stream
+    t = N.table_arg(PatchQuant(1.0).get_quantization_table())
+    F, H, W = 256, 2160, 3840
+    img = B.intra_frames(F, H, W, seed=3, dev=dev)
+    q = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+    N.check(L.ivc_intra_encode_dev(img.data_ptr(), 1, F, H, W, 1, t.ctypes.data, N.F64, 1,
+                                   q.data_ptr(), None, 0, 0, stream))
+    nblk = q.numel() // 64
+    off = torch.empty(nblk + 1, dtype=torch.int64, device=dev)
+    one = torch.empty(1, dtype=torch.int32, device=dev)
+    N.check(L.ivc_zerorun_encode_dev(q.data_ptr(), nblk, 64, 64, 4000, off.data_ptr(),
+                                     one.data_ptr(), 0, stream))
+    nsym = int(off[-1].item())
+    ref = torch.empty(nsym, dtype=torch.int32, device=dev)
+    N.check(L.ivc_zerorun_encode_dev(q.data_ptr(), nblk, 64, 64, 4000, off.data_ptr(),
+                                     ref.data_ptr(), nsym, stream))
+    work = torch.empty_like(ref)
+    nsd = torch.zeros(1, dtype=torch.int64, device=dev)
+    hist = torch.zeros(8194, dtype=torch.int64, device=dev)
+    rgb = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
+    err = torch.zeros(3, dtype=torch.int64, device=dev)
+    hist_ref = rgb_ref = None
+    bad = 0
+    for rep in range(args.reps):
+        hist.zero_()
+        N.check(L.ivc_intra_symbols_hist_dev(img.data_ptr(), 1, F, H, W, 1, t.ctypes.data, 4000,
+                                             work.data_ptr(), nsym, nsd.data_ptr(),
+                                             hist.data_ptr(), -4097, 8194, stream))
+        ok_s = torch.equal(work, ref) and int(nsd.item()) == nsym
+        N.check(L.ivc_zerorun_encode_dev(q.data_ptr(), nblk, 64, 64, 4000, off.data_ptr(),
+                                         work.data_ptr(), nsym, stream))
+        ok_z = torch.equal(work, ref)
+        N.check(L.ivc_symbols2image_dev(ref.data_ptr(), nsym, F, H, W, 3, t.ctypes.data, 4000, 1,
+                                        rgb.data_ptr(), err.data_ptr(), stream))
+        torch.cuda.synchronize()
+        if rep == 0:
+            hist_ref, rgb_ref = hist.clone(), rgb.clone()
+        ok_h = torch.equal(hist, hist_ref)
+        ok_d = torch.equal(rgb.view(torch.int64), rgb_ref.view(torch.int64)) and int(err[0]) == 0
+        ok = ok_s and ok_z and ok_h and ok_d
+        if not args.quiet or not ok:
+            print(f"rep {rep}: image2symbols {'ok' if ok_s else 'DIFF'}  zerorun {'ok' if ok_z else 'DIFF'}  "
+                  f"hist {'ok' if ok_h else 'DIFF'}  symbols2image {'ok' if ok_d else 'DIFF'}", flush=True)
+        if not ok_d:
+            ne = (rgb.view(torch.int64) != rgb_ref.view(torch.int64)).any(-1).nonzero()
+            print(f"  symbols2image: {ne.shape[0]} pixels differ, first {ne[:6].tolist()}", flush=True)
+        bad += not ok
+    print(f"mode intra lib {args.lib or 'in-tree'}: {bad} of {args.reps} runs differ", flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=12)
@@ -67,6 +122,8 @@ def main():
                 fn.argtypes, fn.restype = a, r
         N._lib = L
     dev = torch.device("cuda", 0)
+    if args.mode == "intra":
+        return intra(args, dev)
     F, H, W, sr = args.frames, 4320, 7680, 16
     table = PatchQuant(1.0).get_quantization_table()
     seq = B.inter_frames(F, H, W, seed=5, dev=dev)

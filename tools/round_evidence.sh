@@ -16,6 +16,7 @@ if [ -z "$SKIP_TESTS" ]; then
   echo smoke ok
   # the cfg5 step repeated against an unchunked single-stream run, bitwise (the r05 LDS race)
   timeout -k 10 300 python -u tools/race_probe.py --reps 300 --quiet > gpurun_out/race_probe_$TAG.log 2>&1 || { tail -20 gpurun_out/race_probe_$TAG.log; exit 1; }
+  timeout -k 10 300 python -u tools/race_probe.py --mode intra --reps 60 --quiet >> gpurun_out/race_probe_$TAG.log 2>&1 || { tail -20 gpurun_out/race_probe_$TAG.log; exit 1; }
   grep "runs differ" gpurun_out/race_probe_$TAG.log
 fi
 timeout -k 10 900 python bench.py ${BENCH_ARGS} > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 1; }
