@@ -53,6 +53,9 @@ constexpr int DX_WAVE = 8 * 72;  // doubles per wave: transpose image [b][k pitc
 #ifndef IVC_DEC_PAD_ZERO
 #define IVC_DEC_PAD_ZERO 1       // sym_image_kernel: no per-symbol bound test (see the parse)
 #endif
+#ifndef IVC_DEC_FOLD16
+#define IVC_DEC_FOLD16 1         // sym_image_kernel, DQ_INT: the 1/16 scaling folded into the table
+#endif
 // ablation builds only (tools/ab), bits: 1 = the image stores skipped (behind a runtime test the
 // compiler cannot fold), 2 = sym_image_kernel's parse skipped (the staging stays zero)
 #ifndef IVC_DEC_ABLATE
@@ -148,8 +151,10 @@ __device__ __forceinline__ void dec_group_math(const DecArgs& a, const DecGroup&
     for (int i = 0; i < 8; ++i) x[i] = xs[b * 72 + i * 9 + r];
     __builtin_amdgcn_wave_barrier();
     dct3_line<double>(x, 1.0, true);                  // axis -2 (column r)
+    if constexpr (!(DQM == DQ_INT && IVC_DEC_FOLD16)) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = x[i] * 0.0625;
+      for (int i = 0; i < 8; ++i) x[i] = x[i] * 0.0625;
+    }
     if constexpr (OUTL == DEC_BLOCKS) {
       // plane p of the group's blocks: [b][i][r], 8 x 512 B, block b's plane at
       // out + ((blk0 + b) * 3 + p) * 64
@@ -319,7 +324,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int b = lane >> 3, r = lane & 7;
-  for (int i = tid; i < 192; i += 256) tq[i] = t.q[i];
+  // DQ_INT: q * table is an exact integer, so q * (table / 16) = (q * table) / 16 exactly and
+  // the IDCT's 1/16 rides in the table (IVC_DEC_FOLD16: 24 float64 multiplies per lane and group)
+  for (int i = tid; i < 192; i += 256) tq[i] = (DQM == DQ_INT && IVC_DEC_FOLD16) ? t.q[i] * 0.0625 : t.q[i];
   uint32_t pos[2];
   dec_gather_pos<true>(r, pos);
   lds_barrier();   // the table only
