@@ -391,6 +391,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void s
       for (int c0 = 0; c0 < rlen; c0 += 256) {
         const int i0 = c0 + 4 * lane;
         const dec_u32x4 q = *reinterpret_cast<const dec_u32x4*>(st + i0);
+        // (the neighbours from the neighbouring lanes by DPP wave shifts instead — these strided
+        // reads are 4-way bank conflicts — measured 0.2 % slower, profiles/r05an_*)
         const int pvs = st[i0 - 1], nxs = st[i0 + 4];
         const int v[4] = {(int)q.x, (int)q.y, (int)q.z, (int)q.w};
         int pk[4];
