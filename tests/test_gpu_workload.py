@@ -237,6 +237,30 @@ def test_chunked_inter_encode_with_side_stream_histograms():
     assert_bits(q2[3], wq.reshape(H // 8, W // 8, 3, 64), "q pair 3")
 
 
+def test_me_matrix_core_search_repeatable():
+    """The +-16 matrix-core search relaunched many times over 16 8K pairs (the persistent grid
+    walks ~15 tiles per workgroup, so every workgroup crosses its loop-header barrier many
+    times) gives the same vectors every time: before every barrier drained its LDS writes
+    (ivc_internal.h lds_barrier) the cross-wave merge read a stale per-wave entry in ~4 % of
+    cfg5 steps (profiles/r05ai_race_probe.log).  A guard, not a proof: a rare race can pass."""
+    dev = torch.device("cuda:0")
+    F, H, W, sr = 17, 4320, 7680, 16
+    seq = bench.inter_frames(F, H, W, seed=5, dev=dev)
+    mv = torch.empty((F - 1, H // 8, W // 8), dtype=torch.int64, device=dev)
+    D.motion_estimate(seq[:-1], seq[1:], sr, mv, exact_u8=True)
+    ref = mv.clone()
+    differ = 0
+    for _ in range(60):
+        mv.fill_(-1)
+        D.motion_estimate(seq[:-1], seq[1:], sr, mv, exact_u8=True)
+        differ += not torch.equal(mv, ref)
+    assert differ == 0, f"{differ} of 60 relaunches gave different motion vectors"
+    # and one block-row stripe of pair 0 against the C oracle
+    host = seq[:2].cpu().numpy()
+    wmv, _ = c_inter_encode(host[0], host[1], sr, 1.0, rows=(0, 3))
+    assert_bits(ref[0, 0:3].cpu().numpy(), wmv[..., 0], "mv pair 0 rows 0-2")
+
+
 @pytest.mark.parametrize("C,chunks", [(3, None), (1, None), (3, 3), (1, 16)])
 def test_symbols2image_fused_adversarial(tune, C, chunks):
     """The fused symbols -> image kernel (ivc_decode.hip sym_image_kernel: zero-run expansion
