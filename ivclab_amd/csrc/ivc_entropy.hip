@@ -1486,15 +1486,16 @@ __global__ void s2i_rejected_verdict(const int* ok, int64_t* err) {
 // as chunk j's starts are known (its last group ends in chunk j) — so the stream pass of chunk
 // j + 1 overlaps the decode of chunk j - 1 (the decode leaves VGPRs and wave slots for it).
 #ifndef IVC_S2I_CHUNKS
-#define IVC_S2I_CHUNKS 32
-#endif
+#define IVC_S2I_CHUNKS 64        // with the 13 K-tile minimum: cfg3 (865 K tiles) in 64 chunks,
+#endif                           // 64 frames in 16 (r05: 15.30 -> 15.13 and 3.918 -> 3.890 ms
+                                 // against 32 / 16 K, profiles/r05ar_ab_decode_chunking.log)
 #ifndef IVC_S2I_COUNT_WGCU
 #define IVC_S2I_COUNT_WGCU 2     // the pipelined call's EOB pass: workgroups per CU (2: 14.89,
                                  // 4: 14.93, 6: 17.47 (the streams serialise), 8: 15.08 ms,
                                  // profiles/r05ab_ab_decode_count_grid.log)
 #endif
 #ifndef IVC_S2I_MIN_CHUNK
-#define IVC_S2I_MIN_CHUNK 16384
+#define IVC_S2I_MIN_CHUNK 13312
 #endif
 static int s2i_chunks(int64_t ntf) {
   // ivc_set_tuning(IVC_TUNE_S2I_CHUNKS, K) pipelines any stream of >= K tiles
