@@ -59,18 +59,31 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
-# VALU peaks, 256 CUs x 4 SIMDs x 64 lanes at 2.4 GHz:
+# One clock for every compute peak: the guide's max clock, 2.4 GHz (MI355X_MICROARCH.md
+# "Max clock"), over 256 CUs x 4 SIMDs.
+CLOCK_HZ = 2.4e9
+SIMDS = 256 * 4
+# VALU peaks, 1024 SIMDs x 64 lanes:
 #   v_dot4_u32_u8 issues at half rate (tools/ubench/valu_rates.hip): 39.3 T lane-instr/s
 #   FP64 add/mul (no FMA: NumPy rounds every product): half the FP32 vector rate, 39.3 T op/s
-DOT4_PEAK_T = 256 * 4 * 64 * 2.4e9 / 4 / 1e12
-# issue roofline of the +-16 matrix-core search (leg_inter): per-tile instruction counts from
-# its PMC (profiles/r05_pmc_me.json), issue costs and capacity as in leg_inter
+DOT4_PEAK_T = SIMDS * 64 * CLOCK_HZ / 4 / 1e12
+# Issue model of the +-16 matrix-core search (leg_inter), the guide's cycle constants
+# (MI355X_MICROARCH.md, "Per-instruction cycle constants"): a wave64 VALU instruction occupies
+# its SIMD's vector issue for 2 cycles (throughput, several waves); v_mfma_i32_16x16x64_i8 takes
+# the cycles of the bf16 16x16x32 form, 16 per SIMD, of which it holds the SIMD's vector issue
+# for 8 ("an MFMA holds the SIMD's vector issue for ... 8 of its 16"; costs add).  So per SIMD:
+#   vector issue = 2 VALU + 8 MFMA cycles,  matrix pipe = 16 MFMA cycles,
+# and the kernel is bound by the larger.  Per-tile counts from its PMC (profiles/r05_pmc_me.json).
 ME_VALU_PER_TILE, ME_MFMA_PER_TILE = 2843, 246
-VALU_ISSUE_CYC, MFMA_ISSUE_CYC = 2.49, 8
-ISSUE_PEAK_T = 256 * 4 * 2.1e9 / 1e12
-# dense i8 MFMA: twice the bf16 rate (MI355X_MICROARCH.md: ~2.5 PF bf16 dense)
-MFMA_I8_PEAK_T = 5000.0
+ME_PMC_SOURCE = "profiles/r05_pmc_me.json"
+VALU_CYC, MFMA_I8_CYC, MFMA_VALU_HOLD_CYC = 2, 16, 8
+ISSUE_PEAK_T = SIMDS * CLOCK_HZ / 1e12          # T SIMD-cycles/s
+# dense i8 MFMA: 16x16x64 = 32768 ops per 16 cycles per SIMD = 5.03 P op/s (2x bf16 per clock)
+MFMA_I8_PEAK_T = 16 * 16 * 64 * 2 / MFMA_I8_CYC * SIMDS * CLOCK_HZ / 1e12
 F64_PEAK_T = 78.6 / 2
+# per 8-block x 3-plane group of sym_image_kernel (the fused decode), from its PMC
+DEC_PER_GROUP = {"valu": 976.5, "f64_add_mul": 276.0 + 164.0, "cvt": 24.1}
+DEC_PMC_SOURCE = "profiles/r05_pmc_decode.json"
 HIST_LO, HIST_BINS = -4096, 8192
 PACE_MARGIN = 0.02             # settle the store pace this far below its lowest failed rate
 METRIC = "Mpixels/s: 4K intra DCT+quant and ±16 full-search ME, 1/2/4/8 MI355X"
@@ -264,56 +277,98 @@ def csrc_sha256():
 
 
 # ---------------------------------------------------------------- HBM traffic (PMC) -----
-INTRA_KERNEL_MATCH = "fused_encode_kernel<unsigned char, double, double, 1,"
+
+
+PMC_CALLS = 2                   # calls of the measured op per --pmc-child run
 
 
 def pmc_child(args):
-    """--pmc-child: the headline kernel alone on the bench workload (same frames, same output
-    buffer shape), launched twice; run under `rocprofv3 --pmc <counter>` by pmc_traffic."""
+    """--pmc-child MODE: one op of the bench on its bench workload (same generator, same sizes),
+    launched PMC_CALLS times; run under `rocprofv3 --pmc <counter>` by pmc_traffic.
+      intra    the headline kernel (fused patch -> DCT -> quant, 3 int32 planes)
+      symbols  pixels -> zero-run symbols with the emission pass's histogram (the
+               image2symbols leg: count pass, scans, emitter, histogram gate)
+      zerorun  ZeroRunCoder.encode of the zig-zag coefficients (count pass, scans, emitter);
+               the coefficients are made first by the intra kernel, which pmc_traffic excludes
+    `--pmc-nsym` sizes the symbol buffer (the parent knows the stream length)."""
     import ivclab_amd.device as D
     from ivclab_amd import PatchQuant
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     F, H, W = args.frames, args.height, args.width
     frames = intra_frames(F, H, W, seed=3, dev=dev).view(F, H, W, 1)
-    out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
     table = PatchQuant(1.0).get_quantization_table()
-    for _ in range(2):
-        D.intra_encode(frames, table, out, zigzag=args.zigzag)
+    mode = args.pmc_child
+    if mode == "intra":
+        out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+        for _ in range(PMC_CALLS):
+            D.intra_encode(frames, table, out, zigzag=args.zigzag)
+    elif mode == "symbols":
+        sym = torch.empty(args.pmc_nsym, dtype=torch.int32, device=dev)
+        nsym_d = torch.zeros(1, dtype=torch.int64, device=dev)
+        hist = torch.zeros(HIST_BINS + 2, dtype=torch.int64, device=dev)
+        for _ in range(PMC_CALLS):
+            hist.zero_()
+            D.intra_symbols(frames, table, sym, nsym_d, hist=hist, hist_lo=HIST_LO - 1)
+    elif mode == "zerorun":
+        out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
+        D.intra_encode(frames, table, out, zigzag=True)
+        del frames
+        blocks = out.view(-1, 64)
+        offs = torch.empty(blocks.shape[0] + 1, dtype=torch.int64, device=dev)
+        sym = torch.empty(args.pmc_nsym, dtype=torch.int32, device=dev)
+        for _ in range(PMC_CALLS):
+            D.zerorun_encode(blocks, offs, sym)
+    else:
+        raise SystemExit(f"--pmc-child: unknown mode {mode!r}")
     torch.cuda.synchronize()
 
 
-def _pmc_counter_mean(root, counter, match):
-    """Mean per-dispatch value of `counter` over the dispatches of kernels whose name contains
-    `match`, from a rocprofv3 --pmc CSV output directory."""
+def _pmc_counter_total(root, counter, match, exclude=None):
+    """Sum of `counter` over the dispatches of kernels whose name contains `match` (and not
+    `exclude`), from a rocprofv3 --pmc CSV output directory; returns (sum, dispatches)."""
     import csv
     import glob
     per = {}
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if match in r.get("Kernel_Name", "") and r.get("Counter_Name") == counter:
+                name = r.get("Kernel_Name", "")
+                if (match in name and (exclude is None or exclude not in name)
+                        and r.get("Counter_Name") == counter):
                     per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
-    return (sum(per.values()) / len(per), len(per)) if per else (None, 0)
+    return (sum(per.values()), len(per)) if per else (None, 0)
 
 
-def pmc_traffic(args, timeout_s=150):
-    """HBM bytes per launch of the headline kernel, measured on this box during the bench:
-    two child processes (`rocprofv3 --pmc FETCH_SIZE`, then `--pmc WRITE_SIZE`: they do not
-    fit one pass) each running --pmc-child under its own kill timer.  Corrections as
-    MI355X_MICROARCH.md's HBM/rocprofv3 section prescribes: the counters are KiB; on gfx950
-    FETCH_SIZE reports half the bytes of a wide (16 B/lane) streaming read, so it is doubled;
-    WRITE_SIZE is exact for 16 B/lane stores.  Returns (bytes or None, detail dict)."""
+PMC_MODES = {                    # mode: (kernel-name match, exclude)
+    "intra": ("fused_encode_kernel<unsigned char, double, double, 1,", None),
+    "symbols": ("ivc::", None),
+    "zerorun": ("ivc::", "fused_encode_kernel"),
+}
+
+
+def pmc_traffic(args, mode="intra", nsym=0, timeout_s=150):
+    """HBM bytes per call of one op, measured on this box during the bench: two child
+    processes (`rocprofv3 --pmc FETCH_SIZE`, then `--pmc WRITE_SIZE`: they do not fit one
+    pass) each running --pmc-child MODE under its own kill timer; the bytes of every dispatch
+    of the op's kernels summed and divided by the calls.  Corrections as MI355X_MICROARCH.md's
+    HBM/rocprofv3 section prescribes: the counters are KiB; on gfx950 FETCH_SIZE reports half
+    the bytes of a wide (16 B/lane) streaming read, so it is doubled; WRITE_SIZE is exact for
+    16 B/lane stores (the symbols / zero-run kernels also read and write narrower words: the
+    guide calls those widths uncalibrated, so their totals carry that caveat).  Returns
+    (bytes or None, detail dict)."""
     import shutil
     import tempfile
     prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     if not os.path.exists(prof):
         return None, {"error": "rocprofv3 not found"}
-    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", "--frames", str(args.frames),
-             "--height", str(args.height), "--width", str(args.width)] + (["--zigzag"] if args.zigzag else [])
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", mode, "--frames", str(args.frames),
+             "--height", str(args.height), "--width", str(args.width),
+             "--pmc-nsym", str(int(nsym))] + (["--zigzag"] if args.zigzag else [])
     env = dict(os.environ, TMPDIR="/tmp")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
+    match, exclude = PMC_MODES[mode]
     vals, detail = {}, {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="ivc_pmc_", dir="/tmp")
@@ -324,15 +379,15 @@ def pmc_traffic(args, timeout_s=150):
             if r.returncode != 0:
                 return None, {"error": f"{ctr} pass exit {r.returncode}",
                               "stderr_tail": r.stderr.decode(errors="replace")[-300:]}
-            v, n = _pmc_counter_mean(d, ctr, INTRA_KERNEL_MATCH)
+            v, n = _pmc_counter_total(d, ctr, match, exclude)
             if v is None:
-                return None, {"error": f"{ctr}: no dispatch of the kernel in the PMC output"}
-            vals[ctr], detail[f"{ctr}_dispatches"] = v, n
+                return None, {"error": f"{ctr}: no dispatch of the op's kernels in the PMC output"}
+            vals[ctr], detail[f"{ctr}_dispatches"] = v / PMC_CALLS, n
         finally:
             shutil.rmtree(d, ignore_errors=True)
     fetch = 2.0 * vals["FETCH_SIZE"] * 1024
     write = vals["WRITE_SIZE"] * 1024
-    detail.update({"fetch_bytes": round(fetch), "write_bytes": round(write),
+    detail.update({"fetch_bytes": round(fetch), "write_bytes": round(write), "calls": PMC_CALLS,
                    "correction": "FETCH_SIZE x 2 (gfx950 wide-read half count), WRITE_SIZE as is; KiB -> B"})
     return fetch + write, detail
 
@@ -649,6 +704,8 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
         "blocks_per_gpu": nblk, "symbols_per_gpu": nsym, "ms": round(zms, 3),
         "Mblocks_per_s": round(nblk / zms / 1e3, 1),
         "note": "ZeroRunCoder.encode of the zig-zag output (count, scan, emit kernels)",
+        "bound": "issue (emitter VALU/SALU; count pass HBM read), DESIGN.md 5f",
+        "algorithmic_bytes": nblk * 256 + nsym * 4,
         "algorithmic_GBs": round((nblk * 256 + nsym * 4) / (zms * 1e-3) / 1e9, 1)}
     result["image2symbols"] = {
         "ms": round(fms, 3), "Mpixels_per_s": round(px_step / fms / 1e3, 1),
@@ -656,6 +713,8 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
         "note": "u8 pixels -> DCT -> quant -> zig-zag -> zero-run symbols fused (count pass + "
                 "scan + emit pass); algorithmic bytes = the pixels once (1 B/px) + the stream "
                 "(4 B/symbol): the int8 hand-off between the passes is the implementation's",
+        "bound": "issue (count pass fp64 VALU; emitter VALU/SALU), DESIGN.md 5d",
+        "algorithmic_bytes": px_step * 1 + nsym * 4,
         "algorithmic_GBs": round((px_step * 1 + nsym * 4) / (fms * 1e-3) / 1e9, 1)}
     if verify is not None and dist is None:
         # against the two-pass form (exact min/max, then the histogram over those bounds: the
@@ -711,12 +770,27 @@ def leg_decode(args, dist, rank, world, dev, table, out, sym, result, verify):
     # the fused path: the stream read once (4 B/symbol) + RGB float64 out (24 B/px), over the
     # whole symbols2image call (EOB count pass + scan + group locate + fused kernel)
     salgo = int(sym.numel()) * 4 + px * 24
+    # issue floor of the fused decode kernel (sym_image_kernel): its per-group instruction mix
+    # from PMC (DEC_PER_GROUP) at the guide's issue costs — 4 cycles per wave64 float64
+    # add/mul/cvt (half the FP32 vector rate: 78.6 TF FP64 = 16 lanes per SIMD-cycle), 2 per
+    # other VALU — over 1024 SIMDs x 2.4 GHz; the scalar unit issues beside the VALU
+    groups = F * h * ((w + 7) // 8)
+    f64n = DEC_PER_GROUP["f64_add_mul"] + DEC_PER_GROUP["cvt"]
+    dec_cyc = groups * (f64n * 4 + (DEC_PER_GROUP["valu"] - f64n) * 2)
+    dec_floor_ms = dec_cyc / (SIMDS * CLOCK_HZ) * 1e3
     result["decode"] = {
         "metric": "Mpixels/s: IntraCodec.symbols2image of the cfg3 stream (3-plane YCbCr -> RGB float64)",
         "value": round(world * px / sms / 1e3, 1), "unit": "Mpixels/s", "ms": round(sms, 3),
         "symbols_per_gpu": int(sym.numel()),
-        "roofline": {"bound": "hbm", "kernel": "symbols2image (zf_count + scan + sym_locate + "
-                                               "sym_image_kernel<3,rgb>)",
+        "roofline": {"bound": "issue/latency (fp64 IDCT + parse VALU at 4 waves/SIMD; DESIGN.md 5e)",
+                     "kernel": "symbols2image (zf_count + scan + sym_locate + "
+                               "sym_image_kernel<3,rgb>)",
+                     "issue_floor_ms": round(dec_floor_ms, 3),
+                     "issue_floor_frac": round(dec_floor_ms / sms, 4),
+                     "issue_floor_note": (f"sym_image_kernel's VALU at the guide's issue costs: "
+                                          f"{groups} groups x ({f64n:.0f} float64 x 4 + "
+                                          f"{DEC_PER_GROUP['valu'] - f64n:.0f} other x 2 cycles) / "
+                                          f"(1024 SIMDs x 2.4 GHz); counts {DEC_PMC_SOURCE}"),
                      "ms": round(sms, 4), "achieved": round(salgo / (sms * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(salgo / (sms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -763,14 +837,15 @@ def leg_inter(args, dist, rank, world, dev, table, result, verify):
     ipx = (Fi - 1) * Hi * Wi
     cand = valid_candidates(Hi, Wi, sr) * (Fi - 1)
     macs = cand * 64                        # useful multiply-adds (window x block) per search
-    # issue roofline of me_mfma16x2_kernel (the counters show its VALU issue, not the matrix
-    # cores, binding: profiles/r05_pmc_me.json): per tile of 2 x 8 blocks the kernel issues
-    # ME_VALU_PER_TILE vector and ME_MFMA_PER_TILE v_mfma_i32_16x16x64_i8 instructions (static
-    # per tile: no data-dependent branches); a wave64 integer VALU instruction costs its SIMD
-    # 2.49 issue cycles at full occupancy (tools/ubench/valu_rates.hip), an MFMA holds the SIMD's
-    # vector issue for 8 (MI355X guide, cycle constants); capacity = 1024 SIMDs x 2.1 GHz
+    # issue roofline of me_mfma16x2_kernel (the counters show its vector issue, not the
+    # matrix cores, binding): per tile of 2 x 8 blocks the kernel issues ME_VALU_PER_TILE vector
+    # and ME_MFMA_PER_TILE v_mfma_i32_16x16x64_i8 instructions (static per tile: no
+    # data-dependent branches); cycle constants and capacity: the header (one 2.4 GHz clock)
     tiles = (Fi - 1) * ((Hi // 8 + 1) // 2) * ((Wi // 8 + 7) // 8)
-    issue = tiles * (ME_VALU_PER_TILE * VALU_ISSUE_CYC + ME_MFMA_PER_TILE * MFMA_ISSUE_CYC)
+    cap = (me_ms * 1e-3) * SIMDS * CLOCK_HZ            # SIMD-cycles in the kernel's time
+    valu_cyc = tiles * ME_VALU_PER_TILE * VALU_CYC
+    mfma_pipe = tiles * ME_MFMA_PER_TILE * MFMA_I8_CYC
+    vec_issue = valu_cyc + tiles * ME_MFMA_PER_TILE * MFMA_VALU_HOLD_CYC
     live_ops = tiles * ME_MFMA_PER_TILE * 16 * 16 * 64 * 2     # every MFMA output, live or masked
     dot4 = cand * 16
     result["inter"] = {
@@ -779,24 +854,33 @@ def leg_inter(args, dist, rank, world, dev, table, result, verify):
         "ms_per_step": round(iwall / args.inter_steps * 1e3, 3),
         "config": {"workload": f"cfg4: {Fi} frames 1920x1080 u8 luma per GPU, sr={sr}, "
                                "ME against the previous source frame (open loop)"},
-        "roofline": {"bound": "issue (VALU + MFMA issue slots; PMC)",
+        "roofline": {"bound": "vector issue (VALU + the MFMA's issue hold; PMC counts, guide cycles)",
                      "kernel": "me_mfma16x2_kernel",
                      "kernel_ms": round(me_ms, 4),
-                     "achieved": round(issue / (me_ms * 1e-3) / 1e12, 4),
+                     "achieved": round(vec_issue / (me_ms * 1e-3) / 1e12, 4),
                      "peak": round(ISSUE_PEAK_T, 4), "unit": "T SIMD issue-cycles/s",
-                     "frac": round(issue / (me_ms * 1e-3) / 1e12 / ISSUE_PEAK_T, 4),
-                     "issue_cycles_per_launch": issue, "tiles_per_launch": tiles,
+                     "frac": round(vec_issue / cap, 4),
+                     "valu_issue_frac": round(valu_cyc / cap, 4),
+                     "mfma_pipe_frac": round(mfma_pipe / cap, 4),
+                     "cycles_per_launch": {"valu": valu_cyc, "mfma_pipe": mfma_pipe,
+                                           "vector_issue": vec_issue},
+                     "tiles_per_launch": tiles,
                      "per_tile": {"valu": ME_VALU_PER_TILE, "mfma": ME_MFMA_PER_TILE,
-                                  "source": "profiles/r05_pmc_me.json (SQ_INSTS_VALU - "
+                                  "source": ME_PMC_SOURCE + " (SQ_INSTS_VALU - "
                                             "SQ_INSTS_VALU_MFMA_I8, SQ_INSTS_MFMA per dispatch / tiles)"},
+                     "constants": {"clock_GHz": CLOCK_HZ / 1e9, "simds": SIMDS,
+                                   "valu_cyc": VALU_CYC, "mfma_i8_16x16x64_cyc": MFMA_I8_CYC,
+                                   "mfma_vector_issue_hold_cyc": MFMA_VALU_HOLD_CYC,
+                                   "source": "MI355X_MICROARCH.md per-instruction cycle constants"},
                      "mfma_i8": {"useful_TOPs": round(2 * macs / (me_ms * 1e-3) / 1e12, 1),
                                  "live_TOPs": round(live_ops / (me_ms * 1e-3) / 1e12, 1),
-                                 "peak_TOPs": MFMA_I8_PEAK_T,
+                                 "peak_TOPs": round(MFMA_I8_PEAK_T, 1),
                                  "frac_useful": round(2 * macs / (me_ms * 1e-3) / 1e12 / MFMA_I8_PEAK_T, 4),
                                  "frac_live": round(live_ops / (me_ms * 1e-3) / 1e12 / MFMA_I8_PEAK_T, 4)},
-                     "note": ("frac = the kernel's VALU + MFMA issue cycles over the chip's issue "
-                              "capacity; the matrix cores run at mfma_i8.frac_live (all computed "
-                              "outputs, of which the block's 33 x 33 candidates are 34 %); "
+                     "note": ("frac = vector-issue cycles (2 per VALU + 8 per MFMA) over 1024 SIMDs x "
+                              "2.4 GHz; valu_issue_frac and mfma_pipe_frac (16 per MFMA) are the two "
+                              "pipes apart; the block's 33 x 33 candidates are 34 % of the computed "
+                              "outputs; "
                               f"dot4-equivalent rate (valid candidates x 16 v_dot4 lane-ops against "
                               f"the half-rate dot4 peak, the r02-r04 scale): "
                               f"{dot4 / (me_ms * 1e-3) / 1e12 / DOT4_PEAK_T:.3f}")},
@@ -1103,6 +1187,58 @@ def leg_sharded(args, dist, rank, world, dev, table, result, verify):
         barrier(dist)
 
 
+# ---------------------------------------------------------------- summary ---------------
+def leg_summary(r):
+    """{leg: [ms, frac, bound, extra]} for every leg that ran: ms = the leg's kernel/call time,
+    frac = its roofline fraction (null where it has none), bound = what DESIGN.md §5's counters
+    show binding ("hbm", "issue", "latency", "pcie", "launch"), extra = the leg's one other
+    number (traffic / algorithmic, a floor, a per-call latency)."""
+    def g(d, *ks):
+        for k in ks:
+            if not isinstance(d, dict) or k not in d:
+                return None
+            d = d[k]
+        return d
+    out = {}
+    rl = r.get("roofline")
+    if rl:
+        out["headline"] = [rl.get("kernel_ms"), rl.get("frac"), "hbm",
+                           {"traffic_x": rl.get("traffic_vs_algorithmic")}]
+    if "luma_only" in r:
+        out["luma_only"] = [g(r, "luma_only", "roofline", "kernel_ms"),
+                            g(r, "luma_only", "roofline", "frac"), "issue", None]
+    for k in ("image2symbols", "zerorun"):
+        if k in r:
+            out[k] = [r[k].get("ms"), None, "issue", {"traffic_x": r[k].get("traffic_vs_algorithmic")}]
+    if "decode" in r:
+        out["decode"] = [r["decode"].get("ms"), g(r, "decode", "roofline", "frac"), "issue",
+                         {"issue_floor_ms": g(r, "decode", "roofline", "issue_floor_ms")}]
+        out["coef_to_image"] = [g(r, "decode", "coefficients_to_image", "kernel_ms"),
+                                g(r, "decode", "coefficients_to_image", "frac"), "hbm", None]
+    if "inter" in r:
+        out["inter_step"] = [r["inter"].get("ms_per_step"), None, "issue", None]
+        out["me_sr16"] = [g(r, "inter", "roofline", "kernel_ms"), g(r, "inter", "roofline", "frac"),
+                          "issue", {"valu": g(r, "inter", "roofline", "valu_issue_frac"),
+                                    "mfma": g(r, "inter", "roofline", "mfma_pipe_frac")}]
+    if "inter_f64" in r:
+        out["me_f64"] = [g(r, "inter_f64", "roofline", "kernel_ms"),
+                         g(r, "inter_f64", "roofline", "frac"), "issue", None]
+    if "cfg2" in r:
+        for k, v in r["cfg2"].items():
+            if isinstance(v, dict) and "roofline" in v:
+                out["cfg2_" + k] = [v["roofline"].get("kernel_ms"), v["roofline"].get("frac"),
+                                    "latency" if v.get("frames", 0) > 1 else "launch", None]
+    if "sharded" in r:
+        out["cfg5_step"] = [r["sharded"].get("ms_per_step"), None, "issue", None]
+    sc = g(r, "class_api", "small_call")
+    if sc:
+        out["small_call_us"] = [sc.get("transform_8x8_us"), None, "launch",
+                                {"quantize": sc.get("quantize_3x8x8_us")}]
+    if "verify" in r:
+        out["verify_ok"] = r["verify"].get("ok")
+    return out
+
+
 # ---------------------------------------------------------------- main ------------------
 def parse(argv=None):
     ap = argparse.ArgumentParser()
@@ -1138,7 +1274,8 @@ def parse(argv=None):
     ap.add_argument("--no-verify", action="store_true", help="skip the oracle checks")
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the in-run rocprofv3 --pmc traffic passes (roofline.traffic)")
-    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-child", nargs="?", const="intra", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-nsym", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--sharded-frames", type=int, default=120)
     ap.add_argument("--sharded-height", type=int, default=4320)
     ap.add_argument("--sharded-width", type=int, default=7680)
@@ -1187,6 +1324,7 @@ def main():
         leg_luma_only(args, dist, rank, world, dev, table, frames, result, verify)
     if not args.no_symbols:
         sym = leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify)
+        nsym_total = int(sym.numel())
         if not args.no_decode:
             leg_decode(args, dist, rank, world, dev, table, out, sym, result, verify)
         del sym
@@ -1253,6 +1391,16 @@ def main():
                                     "kernel on this box during this run (child processes)")
             rl["traffic_vs_algorithmic"] = round(tb / rl["algorithmic_bytes_per_launch"], 4)
         rl["traffic_detail"] = tdet
+        # the two issue-bound stream legs: their HBM bytes per call against the algorithmic
+        # bytes (what the int8 hand-offs between their passes cost)
+        if not args.no_symbols:
+            for leg, mode in (("image2symbols", "symbols"), ("zerorun", "zerorun")):
+                tb, tdet = pmc_traffic(args, mode, nsym=nsym_total)
+                r = result[leg]
+                r["traffic"] = None if tb is None else round(tb)
+                if tb is not None:
+                    r["traffic_vs_algorithmic"] = round(tb / r["algorithmic_bytes"], 4)
+                r["traffic_detail"] = tdet
 
     if verify is not None:
         fails = verify["failures"]
@@ -1264,6 +1412,9 @@ def main():
         result["verify"] = {"ok": fails_all == 0, "failures_rank0": fails,
                             "checked_rank0": verify["checked"]}
     result["bench_wall_s"] = round(time.perf_counter() - t_start, 1)
+    # last key: the driver keeps the line's final ~2000 characters, so every leg's time, roofline
+    # fraction and bound are repeated here in a compact form
+    result["legs"] = leg_summary(result)
     if rank == 0:
         os.write(json_fd, (json.dumps(result) + "\n").encode())
     if dist is not None or FORCE_COLL:

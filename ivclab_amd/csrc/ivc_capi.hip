@@ -202,7 +202,10 @@ constexpr size_t kTinyMax = 64u << 10;      // bytes of input and of output for 
 constexpr size_t kTinyFlag = 2 * kTinyMax;
 bool tiny_ready(DevCtx* c) {
   if (c->tiny_state == 0) {
-    c->tiny_state = hipHostMalloc(&c->tiny, 2 * kTinyMax + 256, hipHostMallocDefault) == hipSuccess ? 1 : -1;
+    // coherent (fine-grained) whatever HIP_HOST_COHERENT says: the host reads the completion
+    // word and the output the kernel released at system scope straight from this block
+    c->tiny_state = hipHostMalloc(&c->tiny, 2 * kTinyMax + 256,
+                                  hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess ? 1 : -1;
     if (c->tiny_state == 1) *reinterpret_cast<volatile uint32_t*>((char*)c->tiny + kTinyFlag) = 0;
     // the finished-workgroup counter of tiny_done (device memory, left at 0 by every call)
     if (c->tiny_state == 1 && (hipMalloc((void**)&c->tiny_count, 4) != hipSuccess ||
@@ -426,20 +429,28 @@ struct Staging {
     if (IB <= (size_t)kTinyInline) {           // the input rides in the kernel arguments
       td.inl = src;
       td.inl_bytes = IB;
+      td.stage = ti;                          // ... or, past the launcher's capacity, in `ti`
     } else if (IB) {
       memcpy(ti, src, IB);
     }
     if (launched(launch(ti, to, ctx->stream, &td), what)) return true;
     bool done = false;
     const auto t0 = std::chrono::steady_clock::now();
+    // busy-spin for the first ~200 us (a tiny call finishes in ~7 us on an idle GPU), then
+    // yield the core between polls while the GPU is busy with other work
+    bool relaxed = false;
     for (uint32_t i = 1;; ++i) {
       if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) {
         done = true;
         break;
       }
-      __builtin_ia32_pause();
-      if ((i & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(50))
-        break;
+      if (relaxed) std::this_thread::yield();
+      else __builtin_ia32_pause();
+      if ((i & 255u) == 0) {
+        const auto dt = std::chrono::steady_clock::now() - t0;
+        if (dt > std::chrono::milliseconds(50)) break;
+        relaxed = dt > std::chrono::microseconds(200);
+      }
     }
     if (!done) {
       hipError_t e = hipStreamSynchronize(ctx->stream);

@@ -77,6 +77,7 @@ struct TinyDone {
   uint32_t seq;
   const void* inl = nullptr;
   size_t inl_bytes = 0;
+  void* stage = nullptr;             // the page-locked input block the kernel reads otherwise
 };
 template <int N>
 struct TinyIn {
@@ -88,7 +89,9 @@ struct TinyIn {
 template <typename TD> struct IsTinyIn : std::false_type {};
 template <int N> struct IsTinyIn<TinyIn<N>> : std::true_type {};
 // launch f(TinyIn<N>) when the call's input travels in the arguments, else f(TinyDone);
-// f returns the launch status
+// f returns the launch status.  An input offered inline but larger than this launcher's N is
+// copied into the page-locked block first, so the kernel never reads a stale block whatever N
+// the launcher chose (tests/test_gpu_parity.py::test_tiny_inline_capacity_mismatch).
 template <int N = kTinyInline, typename F>
 inline hipError_t with_tiny(const TinyDone* d, F&& f) {
   if (d && d->inl && d->inl_bytes <= (size_t)N) {
@@ -99,6 +102,7 @@ inline hipError_t with_tiny(const TinyDone* d, F&& f) {
     __builtin_memcpy(t.in, d->inl, d->inl_bytes);
     return f(t);
   }
+  if (d && d->inl && d->inl_bytes && d->stage) __builtin_memcpy(d->stage, d->inl, d->inl_bytes);
   return f(d ? *d : TinyDone{nullptr, nullptr, 0});
 }
 // the kernel's input: the argument segment's copy for a TinyIn launch

@@ -89,10 +89,19 @@ for mod, name in (('ivclab.signal', 'downsample'), ('ivclab.signal', 'FilterPipe
         raise AssertionError(name)
 try:
     ivclab.signal.downsample
-except ImportError as e:
+except AttributeError as e:               # attribute access: the reason, as an AttributeError
     assert 'outside the MI355X block-codec hot path' in str(e)
 else:
     raise AssertionError('downsample')
+assert hasattr(ivclab.signal, 'downsample') is False       # probes behave as on absent names
+assert getattr(ivclab.image, 'IntraCodecAdaptive', 7) == 7
+import ivclab.signal as S
+try:
+    from ivclab.signal import FilterPipeline as _fp       # from-import of a package attribute
+except ImportError as e:
+    assert 'outside the MI355X block-codec hot path' in str(e)
+else:
+    raise AssertionError('FilterPipeline')
 try:
     ivclab.signal.no_such_name
 except AttributeError as e:

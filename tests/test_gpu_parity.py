@@ -116,6 +116,27 @@ def test_tiny_calls_zero_copy():
         assert_bits(z, O.zigzag_scan(blk.astype(np.int32)), "zigzag_scan")
 
 
+def test_tiny_inline_capacity_mismatch():
+    """Inputs of 513-1536 B through the tiny path (above the one-block DCT launcher's 512 B
+    argument capacity, within the general one's): several blocks per DCT call, float64 stacks
+    to quantise, int32 rows to zig-zag, interleaved with one-block calls so a stale page-locked
+    block would show (with_tiny now stages an input it cannot inline)."""
+    rng = np.random.default_rng(515)
+    pq = PatchQuant(0.75)
+    for i in range(20):
+        one = rng.normal(0, 80, (8, 8))
+        assert_bits(DCT.transform(one), O.dct_transform(one), "one block")
+        for shape, dt in (((2, 8, 8), np.float64), ((3, 8, 8), np.float64), ((5, 8, 8), np.float32),
+                          ((3, 8, 8), np.float32), ((24, 8, 8), np.uint8)):
+            x = (rng.normal(0, 60, shape) if dt != np.uint8 else rng.integers(0, 256, shape)).astype(dt)
+            assert 512 < x.nbytes <= 1536, x.nbytes
+            assert_bits(DCT.transform(x), O.dct_transform(x), f"dct {shape} {dt.__name__}")
+        stk = rng.normal(0, 40, (3, 8, 8))
+        assert_bits(pq.quantize(stk), O.quantize(stk, 0.75), "quantize 1536 B")
+        z = rng.integers(-50, 50, (4, 8, 8)).astype(np.int32)      # 1024 B
+        assert_bits(zigzag_scan(z[i % 4]), O.zigzag_scan(z[i % 4]), "zigzag_scan")
+
+
 def test_tiny_call_fast_paths_match_general_path():
     """The per-block fast paths of DCT.transform / PatchQuant.quantize / dequantize (small
     arrays straight to the C-ABI, cached table) give the general path's bits and the oracle's
