@@ -66,7 +66,11 @@ enum ivc_tuning_key {
   IVC_TUNE_S2I_CHUNKS = 2,       /* symbols -> image (ivc_symbols2image*)                  */
   IVC_TUNE_INTER_CHUNKS = 3,     /* fused inter encode (ivc_inter_encode*)                 */
   IVC_TUNE_S2I_NO_FALLBACK = 4,
-  IVC_TUNE_COUNT = 5
+  /* float64 motion search (ivc_motion_estimate* in IVC_ME_NUMPY mode on float64 frames):
+     1 = without the float32 bound phase (every candidate in float64), 2 = the bound phase
+     defers every round to the float64 search (exercises the deferral path); 0 = pruned */
+  IVC_TUNE_F64_ME = 5,
+  IVC_TUNE_COUNT = 6
 };
 int ivc_set_tuning(int key, int value);
 /* the current override of `key` (0: none), or IVC_E_ARG for an unknown key */

@@ -283,7 +283,8 @@ def empty_like(a) -> np.ndarray:
 
 
 # ivc_set_tuning keys (include/ivc.h enum ivc_tuning_key)
-TUNE = {"zr_chunks": 0, "sym_chunks": 1, "s2i_chunks": 2, "inter_chunks": 3, "s2i_no_fallback": 4}
+TUNE = {"zr_chunks": 0, "sym_chunks": 1, "s2i_chunks": 2, "inter_chunks": 3, "s2i_no_fallback": 4,
+        "f64_me": 5}
 
 
 def set_tuning(name: str, value: int) -> int:

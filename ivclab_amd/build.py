@@ -1,6 +1,6 @@
 """Build libivc.so in-tree for gfx950:  python -m ivclab_amd.build [-v]
 
-hipcc compiles the three HIP translation units into ivclab_amd/_lib/libivc.so.  Flags that
+hipcc compiles the HIP translation units (SOURCES) into ivclab_amd/_lib/libivc.so.  Flags that
 matter for parity: -ffp-contract=off (no fused multiply-add: pocketfft / NumPy round every
 product and sum separately) and no fast-math.
 """
@@ -14,8 +14,10 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "_lib", "libivc.so")
-SOURCES = ["ivc_kernels.hip", "ivc_motion.hip", "ivc_me_mfma.hip", "ivc_entropy.hip", "ivc_decode.hip",
-           "ivc_color.hip", "ivc_huffman.hip", "ivc_capi.hip"]
+SOURCES = ["ivc_kernels.hip", "ivc_motion.hip", "ivc_me_mfma.hip", "ivc_me_f64.hip", "ivc_entropy.hip",
+           "ivc_decode.hip", "ivc_color.hip", "ivc_huffman.hip", "ivc_capi.hip"]
+# per-file code-generation flags (ivc_me_f64.hip's header says why)
+FILE_FLAGS = {"ivc_me_f64.hip": ["-fno-slp-vectorize"]}
 HEADERS = ["ivc_math.h", "ivc_internal.h", os.path.join("..", "..", "include", "ivc.h")]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-function"]
@@ -94,7 +96,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(objdir, exist_ok=True)
     compile_flags = [f for f in FLAGS if f != "-shared"]
     objs = [os.path.join(objdir, os.path.splitext(f)[0] + ".o") for f in SOURCES]
-    jobs = [[hipcc()] + compile_flags + ["-c", "-o", o, os.path.join(CSRC, f)]
+    jobs = [[hipcc()] + compile_flags + FILE_FLAGS.get(f, []) + ["-c", "-o", o, os.path.join(CSRC, f)]
             for f, o in zip(SOURCES, objs)]
     workers = max(1, min(len(jobs), int(os.environ.get("MAX_JOBS", "0") or 0) or os.cpu_count() or 1))
     with ThreadPoolExecutor(workers) as ex:

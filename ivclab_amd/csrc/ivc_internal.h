@@ -248,4 +248,39 @@ hipError_t launch_inter_residual(const uint8_t* frames, int64_t nframes, int64_t
                                  int32_t hist_lo = 0, int32_t hist_n = 0);
 
 
+
+// ---- float motion search geometry (ivc_motion.hip me_flt_kernel, ivc_me_f64.hip) ----
+#ifndef IVC_FLT_DY
+#define IVC_FLT_DY 11
+#endif
+#ifndef IVC_FLT_WGCU
+#define IVC_FLT_WGCU 1     // f64 workgroups per CU (2 needs <= 128 VGPRs: FLT_DY 6)
+#endif
+constexpr int FLT_WG = 512, FLT_DY = IVC_FLT_DY;
+
+// Round geometry: NBR blocks per round (2sr+1 threads each), capped so that the window, the
+// blocks and the minimum arrays fit FLT_LDS bytes (the default per-workgroup LDS limit).
+constexpr int FLT_LDS = 64 * 1024;
+template <typename T, int SR> struct FltGeom {
+  // WR window rows plus the rows a partial last dy run reads past them (zeros, never used)
+  static constexpr int N = 2 * SR + 1, WR = 8 + 2 * SR;
+  static constexpr int RUNS = (N + FLT_DY - 1) / FLT_DY, WRP = RUNS * FLT_DY + 7;
+  // a block's 64 pixels at a pitch 16 B past 64 elements: the blocks a half-wave's 16-byte
+  // reads broadcast from then start on different banks
+  static constexpr int CBP = 64 + 16 / (int)sizeof(T);
+  static constexpr int PER_NB = (WRP * 8 + CBP) * (int)sizeof(T) + (int)sizeof(T) + 4;
+  static constexpr int NB_LDS = (FLT_LDS - WRP * 2 * SR * (int)sizeof(T)) / PER_NB;
+  static constexpr int NBR = FLT_WG / N < NB_LDS ? FLT_WG / N : NB_LDS;
+  static constexpr int WC = NBR * 8 + 2 * SR;
+  static constexpr size_t LDS = ((size_t)WRP * WC + (size_t)NBR * CBP) * sizeof(T) +
+                                (size_t)NBR * (sizeof(T) + 4);
+  static_assert(NBR >= 1 && LDS <= (size_t)FLT_LDS, "round does not fit the LDS budget");
+};
+
+// The pruned float64 search (ivc_me_f64.hip) of nf frame pairs for sr in {4, 8, 16}: writes
+// mv for the rounds it settles and appends the others to defer (defer[0] = their count, zeroed
+// by the caller) for me_flt_kernel; defer_all appends every round.  False: sr not compiled.
+bool launch_me_f64p(int sr, const double* ref, const double* cur, int64_t nf, int H, int W,
+                    int64_t* mv, uint32_t* defer, int defer_all, hipStream_t s);
+
 }  // namespace ivc

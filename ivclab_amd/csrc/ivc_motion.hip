@@ -181,14 +181,6 @@ __global__ __launch_bounds__(256) void me_generic_kernel(const T* __restrict__ r
 // (SSD, raster index) minimum over its 2sr+1 threads: an LDS atomic minimum of the SSD bits
 // (non-negative doubles order like their bits), a barrier, then the minimum index among the
 // threads holding that SSD — the reference's first strict minimum.
-#ifndef IVC_FLT_DY
-#define IVC_FLT_DY 11
-#endif
-#ifndef IVC_FLT_WGCU
-#define IVC_FLT_WGCU 1     // f64 workgroups per CU (2 needs <= 128 VGPRs: FLT_DY 6)
-#endif
-constexpr int FLT_WG = 512, FLT_DY = IVC_FLT_DY;
-
 template <typename T> struct FltBits;
 template <> struct FltBits<double> {
   typedef unsigned long long U;
@@ -213,30 +205,14 @@ __device__ __forceinline__ void flt_pin(T (&a)[FLT_DY]) {
                      :: "memory");
 }
 
-// Round geometry: NBR blocks per round (2sr+1 threads each), capped so that the window, the
-// blocks and the minimum arrays fit FLT_LDS bytes (the default per-workgroup LDS limit).
-constexpr int FLT_LDS = 64 * 1024;
-template <typename T, int SR> struct FltGeom {
-  // WR window rows plus the rows a partial last dy run reads past them (zeros, never used)
-  static constexpr int N = 2 * SR + 1, WR = 8 + 2 * SR;
-  static constexpr int RUNS = (N + FLT_DY - 1) / FLT_DY, WRP = RUNS * FLT_DY + 7;
-  // a block's 64 pixels at a pitch 16 B past 64 elements: the blocks a half-wave's 16-byte
-  // reads broadcast from then start on different banks
-  static constexpr int CBP = 64 + 16 / (int)sizeof(T);
-  static constexpr int PER_NB = (WRP * 8 + CBP) * (int)sizeof(T) + (int)sizeof(T) + 4;
-  static constexpr int NB_LDS = (FLT_LDS - WRP * 2 * SR * (int)sizeof(T)) / PER_NB;
-  static constexpr int NBR = FLT_WG / N < NB_LDS ? FLT_WG / N : NB_LDS;
-  static constexpr int WC = NBR * 8 + 2 * SR;
-  static constexpr size_t LDS = ((size_t)WRP * WC + (size_t)NBR * CBP) * sizeof(T) +
-                                (size_t)NBR * (sizeof(T) + 4);
-  static_assert(NBR >= 1 && LDS <= (size_t)FLT_LDS, "round does not fit the LDS budget");
-};
-
+// list (optional): rounds to search, list[0] = their count, list[1..] = round indices (the
+// rounds the pruned float64 search deferred, below); null = every round of the batch
 template <typename T, int SR>
 __global__ __launch_bounds__(FLT_WG, sizeof(T) == 8 ? 2 : 4) void me_flt_kernel(const T* __restrict__ ref,
                                                            const T* __restrict__ cur,
                                                            int64_t nframes, int H, int W,
-                                                           int64_t* __restrict__ mv) {
+                                                           int64_t* __restrict__ mv,
+                                                           const uint32_t* __restrict__ list) {
   typedef typename FltBits<T>::U U;
   typedef FltGeom<T, SR> G;
   extern __shared__ __attribute__((aligned(16))) unsigned char flt_smem[];
@@ -247,10 +223,11 @@ __global__ __launch_bounds__(FLT_WG, sizeof(T) == 8 ? 2 : 4) void me_flt_kernel(
   U* kmin = reinterpret_cast<U*>(cb + nbr * G::CBP);      // [nbr]
   unsigned* imin = reinterpret_cast<unsigned*>(kmin + nbr);
   const int segs = (w + nbr - 1) / nbr;
-  const int64_t rounds = nframes * h * segs;
+  const int64_t rounds = list ? (int64_t)list[0] : nframes * h * segs;
   const int tid = threadIdx.x;
   const int sb = tid / n, se = tid - sb * n;              // block of the round, candidate column
-  for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
+  for (int64_t ri = blockIdx.x; ri < rounds; ri += gridDim.x) {
+    const int64_t r = list ? (int64_t)list[1 + ri] : ri;
     const int64_t f = r / ((int64_t)h * segs);
     const int rem = (int)(r - f * h * segs), by = rem / segs, bx0 = (rem - by * segs) * nbr;
     const int nb = w - bx0 < nbr ? w - bx0 : nbr;
@@ -343,9 +320,35 @@ static void launch_me_flt_sr(const T* ref, const T* cur, int64_t nframes, int64_
   const int w = (int)(W / 8), h = (int)(H / 8);
   const int64_t rounds = nframes * h * ((w + G::NBR - 1) / G::NBR);
   const size_t lds = G::LDS;
+  if constexpr (sizeof(T) == 8) {
+    // the pruned search, then me_flt_kernel on the rounds it deferred (launches of < 2^31
+    // rounds: 32-bit round indices in the list)
+    const int mode = tuning(IVC_TUNE_F64_ME);      // ivc_set_tuning: 1 unpruned, 2 defer all
+    if (rounds > 0 && mode != 1) {
+      const int64_t rpf = (int64_t)h * ((w + G::NBR - 1) / G::NBR);          // rounds per frame
+      const int64_t fmax = (((int64_t)1 << 31) - 1) / rpf;
+      const int64_t chunk = nframes < fmax ? nframes : fmax;
+      uint32_t* defer = nullptr;
+      if (scratch_alloc((void**)&defer, (size_t)(chunk * rpf + 1) * 4, s) == hipSuccess) {
+        const int64_t HW = H * W;
+        for (int64_t f0 = 0; f0 < nframes; f0 += chunk) {
+          const int64_t nf = nframes - f0 < chunk ? nframes - f0 : chunk;
+          (void)hipMemsetAsync(defer, 0, 4, s);
+          const int64_t nr = nf * rpf;
+          launch_me_f64p(SR, (const double*)ref + f0 * HW, (const double*)cur + f0 * HW, nf, (int)H,
+                         (int)W, mv + f0 * h * w, defer, mode == 2, s);
+          me_flt_kernel<T, SR><<<me_grid(nr, 1, IVC_FLT_WGCU), FLT_WG, lds, s>>>(
+              ref + f0 * HW, cur + f0 * HW, nf, (int)H, (int)W, mv + f0 * h * w, defer);
+        }
+        (void)hipFreeAsync(defer, s);
+        return;
+      }
+      (void)hipGetLastError();                   // no scratch: the unpruned search
+    }
+  }
   // f64: 144 VGPRs, one 512-thread workgroup per CU; f32: two (88 VGPRs, LDS permitting)
   const unsigned grid = me_grid(rounds, 1, sizeof(T) == 4 && lds * 2 <= 160 * 1024 ? 2 : IVC_FLT_WGCU);
-  me_flt_kernel<T, SR><<<grid, FLT_WG, lds, s>>>(ref, cur, nframes, (int)H, (int)W, mv);
+  me_flt_kernel<T, SR><<<grid, FLT_WG, lds, s>>>(ref, cur, nframes, (int)H, (int)W, mv, nullptr);
 }
 
 // The float search for the search ranges it is compiled for (window geometry is static, so

@@ -61,7 +61,7 @@ def test_every_compiled_barrier_drains_lds():
 
     def one(src, d):
         out = os.path.join(d, src + ".s")
-        subprocess.run([B.hipcc()] + flags + ["-S", "--cuda-device-only", "-o", out,
+        subprocess.run([B.hipcc()] + flags + B.FILE_FLAGS.get(src, []) + ["-S", "--cuda-device-only", "-o", out,
                                               os.path.join(B.CSRC, src)],
                        check=True, capture_output=True, timeout=600)
         with open(out) as f:

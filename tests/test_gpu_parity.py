@@ -1655,6 +1655,74 @@ def test_me_float_search_kernel(sr, dtype):
             assert_bits(mv, c_motion_vectors(r_, c_, sr), f"{np.dtype(dtype).name} sr={sr} {H}x{W} {what}")
 
 
+def _pairwise_ssd_all(ref, cur, sr, by, bx):
+    """Every in-frame candidate's float64 SSD of block (by, bx) in NumPy's order (the
+    reference's np.sum over the 64 squares), as {raster index: value}."""
+    n, (H, W) = 2 * sr + 1, ref.shape
+    blk = cur[8 * by:8 * by + 8, 8 * bx:8 * bx + 8]
+    out = {}
+    for dy in range(-sr, sr + 1):
+        for dx in range(-sr, sr + 1):
+            y, x = 8 * by + dy, 8 * bx + dx
+            if 0 <= y <= H - 8 and 0 <= x <= W - 8:
+                out[(dy + sr) * n + dx + sr] = np.sum((ref[y:y + 8, x:x + 8] - blk) ** 2)
+    return out
+
+
+def _near_tie_pair(rng, H, W):
+    """Two independent frames of two grey levels mapped through the luma scale of VideoCodec's
+    float64 luma (y = k * 219/255 + 16): every nonzero difference is the same value, so
+    candidates with equal mismatch counts have float64 SSDs that differ only by how the
+    pairwise order rounds their column sums — exact ties and ulp-level near ties at the
+    minimum, which only the exact phase can order."""
+    ref = rng.integers(0, 2, (H, W)) * (219.0 / 255.0) + 16.0
+    cur = rng.integers(0, 2, (H, W)) * (219.0 / 255.0) + 16.0
+    return ref, cur
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_me_f64_pruned_search_exact(mode, tune):
+    """The float64 search with its float32 bound phase (mode 0, the default), without it (1) and
+    with every round deferred to the float64 kernel (2) against the C oracle (NumPy-order SSD,
+    first strict minimum): ulp-level near ties (checked to exist: blocks whose best and
+    runner-up float64 SSDs differ by one to a few ulps), an 8-periodic reference (same squares
+    in every candidate: order decides), a half-flat frame (its rounds overflow the candidate
+    list and are deferred, the others are not), values past 2^24 and below 2^-60 in a few rounds
+    (the bound's assumptions fail: deferred), NaN and inf pixels, and a frame narrower than a
+    round, at sr = 4, 8 and 16."""
+    tune("f64_me", mode)
+    rng = np.random.default_rng(640 + mode)
+    ref, cur = _near_tie_pair(rng, 48, 200)
+    close = ties = 0
+    for by in range(6):
+        for bx in range(25):
+            v = np.array(sorted(_pairwise_ssd_all(ref, cur, 16, by, bx).values()))
+            close += int(0 < v[1] - v[0] <= 4 * np.spacing(v[1]))
+            ties += int(v[1] == v[0])
+    assert close >= 4 and ties >= 10, ("the fixture lacks near ties at the minimum", close, ties)
+    H, W = 72, 264
+    a = rng.normal(128, 50, (H + 40, W + 40))
+    r1, c1 = a[:H, :W].copy(), a[3:H + 3, 5:W + 5] + rng.normal(0, 0.3, (H, W))
+    tile = rng.normal(100, 30, (8, 8))
+    per = np.tile(tile, (H // 8 + 1, W // 8 + 1))[:H, :W]
+    cur_p = np.roll(per, (1, 2), axis=(0, 1)) + 0.37
+    half = r1.copy(); halfc = c1.copy()
+    half[:, :120] = 16.0; halfc[:, :120] = 16.0                 # letterbox-like flat left part
+    big, tiny = r1.copy(), c1.copy()
+    big[8:16, 200:208] *= 2.0 ** 20                              # > 2^24 in one round
+    tiny[40:48, 16:24] = 1e-30                                   # < 2^-60 in another
+    nan = r1.copy()
+    nan[::9, ::11] = np.nan
+    nan[5, :] = np.inf
+    cases = [(ref, cur, "near ties"), (per, cur_p, "periodic"), (half, halfc, "half flat"),
+             (big, c1, "big"), (r1, tiny, "tiny"), (nan, c1, "nan/inf"),
+             (r1[:, :40].copy(), c1[:, :40].copy(), "narrow")]
+    for sr in (4, 8, 16):
+        for r_, c_, what in cases:
+            mv = MotionCompensator(sr).compute_motion_vector(r_, c_)
+            assert_bits(mv, c_motion_vectors(r_, c_, sr), f"mode {mode} sr={sr} {what}")
+
+
 def test_me_float_search_device_frames_and_1080p():
     """Several frame pairs in one device call (rounds over frames), and a full non-integer
     1080p float64 pair at sr = 16 checked on sampled block rows."""

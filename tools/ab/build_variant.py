@@ -19,7 +19,8 @@ objs = [os.path.join(objdir, os.path.splitext(f)[0] + ".o") for f in B.SOURCES]
 csrc = os.environ.get("IVC_CSRC", B.CSRC)
 if csrc != B.CSRC:
     flags += ["-I" + B.CSRC]
-jobs = [[B.hipcc()] + flags + ["-c", "-o", o, os.path.join(csrc, f)] for f, o in zip(B.SOURCES, objs)]
+jobs = [[B.hipcc()] + flags + B.FILE_FLAGS.get(f, []) + ["-c", "-o", o, os.path.join(csrc, f)]
+        for f, o in zip(B.SOURCES, objs)]
 with ThreadPoolExecutor(len(jobs)) as ex:
     list(ex.map(lambda c: B._run(c, False), jobs))
 B._run([B.hipcc(), "--offload-arch=gfx950", "-shared", "-fPIC", "-o",

@@ -35,7 +35,7 @@ def audit(asm):
 
 def one(src, out):
     flags = [f for f in B.FLAGS if f not in ("-shared", "-fPIC")]
-    subprocess.run([B.hipcc()] + flags + ["-S", "--cuda-device-only", "-o", out,
+    subprocess.run([B.hipcc()] + flags + B.FILE_FLAGS.get(src, []) + ["-S", "--cuda-device-only", "-o", out,
                                           os.path.join(B.CSRC, src)], check=True,
                    capture_output=True)
     with open(out) as f:
