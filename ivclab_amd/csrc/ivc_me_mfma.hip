@@ -38,6 +38,11 @@
 
 #include <type_traits>
 
+#ifndef IVC_ME_ABL
+#define IVC_ME_ABL 0   // tools/ab timing builds only (results wrong; profiles/r06f_ab_me_ablation.log):
+                       // 1 no energies, 2 keys of one quad only, 4 no staging writes, 8 no search
+#endif
+
 namespace ivc {
 namespace mf {
 // E's base for a window outside the frame (E in [-671 M, -537 M]), and the least valid key
@@ -131,6 +136,12 @@ __device__ __forceinline__ void me2_search(const uint32_t* lds, int* red, int wa
       const bool top = WV == 0 ? true : (WV == 3 ? dl <= 1 : true);
       const bool bot = WV == 0 ? dl >= 8 : true;
       if (top && q01) acc[0] = max(acc[0], (int)(((uint32_t)d.x << 8) + e));
+      if (IVC_ME_ABL & 2) {
+        acc[1] ^= d.y;
+        acc[2] ^= d.z;
+        acc[3] ^= d.w;
+        continue;
+      }
       if (top && q23) acc[1] = max(acc[1], (int)(((uint32_t)d.y << 8) + e));
       if (bot && q01) acc[2] = max(acc[2], (int)(((uint32_t)d.z << 8) + e));
       if (bot && q23) acc[3] = max(acc[3], (int)(((uint32_t)d.w << 8) + e));
@@ -278,7 +289,7 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
 #pragma unroll
     for (int k = 0; k < IPT; ++k) {
       const int i = ts + 256 * k;
-      if (i < ITEMS) {
+      if (i < ITEMS && !(IVC_ME_ABL & 4)) {
         const int row = i / NPAIR, p = i - row * NPAIR;
         uint32_t* d = lds + row * PITCH + 2 * p;
         const uint32_t w0 = L.raw[k][0] ^ 0x80808080u, w1 = L.raw[k][1] ^ 0x80808080u,
@@ -302,7 +313,7 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
       // (opaque: the per-offset constants derived from u are formed in the tile loop instead of
       // being hoisted out of it, where they stay live — or spill — through the search)
       asm volatile("" : "+v"(u));
-      if (u < U) {
+      if (u < U && !(IVC_ME_ABL & 1)) {
         const uint32_t* cw = lds + (u & 3) * COPY + (u >> 2);
         const int xb = 8 * bx0 - SR, yb = 8 * by - SR;
         const bool xok = xb + u >= 0 && xb + u + 8 <= W;
@@ -336,7 +347,9 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
                               L.bop.z ^ (int)0x80808080u, L.bop.w ^ (int)0x80808080u};
     lds_barrier();
     load(tile + gridDim.x, L);                          // the next tile's inputs, in flight
-    if (wave == 0) me2_search<0>(lds, red, wave, g, l16, bop);
+    if (IVC_ME_ABL & 8) {
+      if (tid < 16) red[2 * tid] = bop.x;
+    } else if (wave == 0) me2_search<0>(lds, red, wave, g, l16, bop);
     else if (wave == 3) me2_search<3>(lds, red, wave, g, l16, bop);
     else me2_search<1>(lds, red, wave, g, l16, bop);
     pf = f;
