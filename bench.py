@@ -59,6 +59,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+HBM_ACHIEVABLE_GBS = 6300.0    # MI355X_MICROARCH.md "HBM": ~6.3 TB/s achievable
 # One clock for every compute peak: the guide's max clock, 2.4 GHz (MI355X_MICROARCH.md
 # "Max clock"), over 256 CUs x 4 SIMDs.
 CLOCK_HZ = 2.4e9
@@ -310,6 +311,21 @@ def pmc_child(args):
         for _ in range(PMC_CALLS):
             hist.zero_()
             D.intra_symbols(frames, table, sym, nsym_d, hist=hist, hist_lo=HIST_LO - 1)
+    elif mode == "decode":
+        # the stream first (pixels -> symbols), then a min/max pass as the marker after which
+        # every ivc:: dispatch is the decode's (the scans are shared by both calls)
+        sym = torch.empty(args.pmc_nsym, dtype=torch.int32, device=dev)
+        nsym_d = torch.zeros(1, dtype=torch.int64, device=dev)
+        D.intra_symbols(frames, table, sym, nsym_d)
+        del frames
+        img = torch.empty((F, H, W, 3), dtype=torch.float64, device=dev)
+        err = torch.zeros(3, dtype=torch.int64, device=dev)
+        mm = torch.empty(2, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        D.minmax(sym, mm)
+        torch.cuda.synchronize()
+        for _ in range(PMC_CALLS):
+            D.symbols2image(sym, 3, table, img, err, to_rgb=True)
     elif mode == "zerorun":
         out = torch.empty((F, H // 8, W // 8, 3, 64), dtype=torch.int32, device=dev)
         D.intra_encode(frames, table, out, zigzag=True)
@@ -324,26 +340,36 @@ def pmc_child(args):
     torch.cuda.synchronize()
 
 
-def _pmc_counter_total(root, counter, match, exclude=None):
+def _pmc_counter_total(root, counter, match, exclude=None, after=None):
     """Sum of `counter` over the dispatches of kernels whose name contains `match` (and not
-    `exclude`), from a rocprofv3 --pmc CSV output directory; returns (sum, dispatches)."""
+    `exclude`; and, given `after`, dispatched after the last kernel whose name contains it),
+    from a rocprofv3 --pmc CSV output directory; returns (sum, dispatches)."""
     import csv
     import glob
-    per = {}
+    rows = []
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         with open(f) as fh:
-            for r in csv.DictReader(fh):
-                name = r.get("Kernel_Name", "")
-                if (match in name and (exclude is None or exclude not in name)
-                        and r.get("Counter_Name") == counter):
-                    per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+            rows += [r for r in csv.DictReader(fh) if r.get("Counter_Name") == counter]
+    mark = -1
+    if after is not None:
+        ids = [int(r["Dispatch_Id"]) for r in rows if after in r.get("Kernel_Name", "")]
+        if not ids:
+            return None, 0
+        mark = max(ids)
+    per = {}
+    for r in rows:
+        name = r.get("Kernel_Name", "")
+        if (match in name and (exclude is None or exclude not in name)
+                and int(r["Dispatch_Id"]) > mark):
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
     return (sum(per.values()), len(per)) if per else (None, 0)
 
 
-PMC_MODES = {                    # mode: (kernel-name match, exclude)
-    "intra": ("fused_encode_kernel<unsigned char, double, double, 1,", None),
-    "symbols": ("ivc::", None),
-    "zerorun": ("ivc::", "fused_encode_kernel"),
+PMC_MODES = {                    # mode: (kernel-name match, exclude, after)
+    "intra": ("fused_encode_kernel<unsigned char, double, double, 1,", None, None),
+    "symbols": ("ivc::", None, None),
+    "zerorun": ("ivc::", "fused_encode_kernel", None),
+    "decode": ("ivc::", None, "minmax_kernel"),
 }
 
 
@@ -368,7 +394,7 @@ def pmc_traffic(args, mode="intra", nsym=0, timeout_s=150):
     env = dict(os.environ, TMPDIR="/tmp")
     for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    match, exclude = PMC_MODES[mode]
+    match, exclude, after = PMC_MODES[mode]
     vals, detail = {}, {}
     for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
         d = tempfile.mkdtemp(prefix="ivc_pmc_", dir="/tmp")
@@ -379,7 +405,7 @@ def pmc_traffic(args, mode="intra", nsym=0, timeout_s=150):
             if r.returncode != 0:
                 return None, {"error": f"{ctr} pass exit {r.returncode}",
                               "stderr_tail": r.stderr.decode(errors="replace")[-300:]}
-            v, n = _pmc_counter_total(d, ctr, match, exclude)
+            v, n = _pmc_counter_total(d, ctr, match, exclude, after)
             if v is None:
                 return None, {"error": f"{ctr}: no dispatch of the op's kernels in the PMC output"}
             vals[ctr], detail[f"{ctr}_dispatches"] = v / PMC_CALLS, n
@@ -782,6 +808,7 @@ def leg_decode(args, dist, rank, world, dev, table, out, sym, result, verify):
         "metric": "Mpixels/s: IntraCodec.symbols2image of the cfg3 stream (3-plane YCbCr -> RGB float64)",
         "value": round(world * px / sms / 1e3, 1), "unit": "Mpixels/s", "ms": round(sms, 3),
         "symbols_per_gpu": int(sym.numel()),
+        "algorithmic_bytes": salgo,
         "roofline": {"bound": "issue/latency (fp64 IDCT + parse VALU at 4 waves/SIMD; DESIGN.md 5e)",
                      "kernel": "symbols2image (zf_count + scan + sym_locate + "
                                "sym_image_kernel<3,rgb>)",
@@ -1231,10 +1258,13 @@ def leg_summary(r):
                             g(r, "luma_only", "roofline", "frac"), "issue", None]
     for k in ("image2symbols", "zerorun"):
         if k in r:
-            out[k] = [r[k].get("ms"), None, "issue", {"traffic_x": r[k].get("traffic_vs_algorithmic")}]
+            out[k] = [r[k].get("ms"), None, "issue", {"traffic_x": r[k].get("traffic_vs_algorithmic"),
+                                                      "floor_ms": r[k].get("traffic_floor_ms")}]
     if "decode" in r:
-        out["decode"] = [r["decode"].get("ms"), g(r, "decode", "roofline", "frac"), "issue",
-                         {"issue_floor_ms": g(r, "decode", "roofline", "issue_floor_ms")}]
+        out["decode"] = [r["decode"].get("ms"), g(r, "decode", "roofline", "frac"), "hbm traffic",
+                         {"traffic_x": r["decode"].get("traffic_vs_algorithmic"),
+                          "floor_ms": r["decode"].get("traffic_floor_ms"),
+                          "issue_floor_ms": g(r, "decode", "roofline", "issue_floor_ms")}]
         out["coef_to_image"] = [g(r, "decode", "coefficients_to_image", "kernel_ms"),
                                 g(r, "decode", "coefficients_to_image", "frac"), "hbm", None]
     if "inter" in r:
@@ -1417,12 +1447,19 @@ def main():
         # the two issue-bound stream legs: their HBM bytes per call against the algorithmic
         # bytes (what the int8 hand-offs between their passes cost)
         if not args.no_symbols:
-            for leg, mode in (("image2symbols", "symbols"), ("zerorun", "zerorun")):
+            legs = [("image2symbols", "symbols"), ("zerorun", "zerorun")]
+            if "decode" in result:
+                legs.append(("decode", "decode"))
+            for leg, mode in legs:
                 tb, tdet = pmc_traffic(args, mode, nsym=nsym_total)
                 r = result[leg]
                 r["traffic"] = None if tb is None else round(tb)
                 if tb is not None:
                     r["traffic_vs_algorithmic"] = round(tb / r["algorithmic_bytes"], 4)
+                    # the call's measured bytes at the chip's achievable HBM rate
+                    # (MI355X_MICROARCH.md: ~6.3 TB/s): its floor as built
+                    r["traffic_floor_ms"] = round(tb / (HBM_ACHIEVABLE_GBS * 1e9) * 1e3, 3)
+                    r["traffic_floor_frac"] = round(r["traffic_floor_ms"] / r["ms"], 4)
                 r["traffic_detail"] = tdet
 
     if verify is not None:

@@ -1358,7 +1358,7 @@ __global__ void zr_decode_verdict_gated(const int32_t* s, const uint8_t* is_rl, 
 }
 
 namespace {
-constexpr int S2I_MAX_CHUNKS = 64;
+constexpr int S2I_MAX_CHUNKS = 256;   // (events reused modulo PIPE_EVENTS - 2: a wait binds at enqueue)
 struct ZrDecScratch {
   uint8_t* is_rl;
   int64_t* agg;
@@ -1545,9 +1545,10 @@ static hipError_t s2i_pipelined(const int32_t* sym, int64_t n, int32_t eob, int6
     if ((e = launch_sym_group_range(z.tile_first, a, b, j == 0, j == K - 1, nframes, H, W, C,
                                     z.grange + 2 * j, s)) != hipSuccess)
       return e;
-    if ((e = hipEventRecord(P.ev[j], s)) != hipSuccess) return e;
+    hipEvent_t evj = P.ev[j % (PIPE_EVENTS - 2)];
+    if ((e = hipEventRecord(evj, s)) != hipSuccess) return e;
     if (j >= 1) {                                  // chunk j - 1's groups end by chunk j's starts
-      if ((e = hipStreamWaitEvent(P.aux, P.ev[j], 0)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(P.aux, evj, 0)) != hipSuccess) return e;
       if ((e = launch_sym_image_range(sym, n, eob, nframes, H, W, C, t, to_rgb, out, z.gstart,
                                       z.flags, z.grange + 2 * (j - 1), P.aux)) != hipSuccess)
         return e;
