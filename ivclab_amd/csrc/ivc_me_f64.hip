@@ -66,6 +66,27 @@ __device__ __forceinline__ float f64p_threshold(float amin, float m) {
   return t;
 }
 
+// The same bound formed in float32: every operation is a sum, product, quotient by a constant
+// or square root of non-negative values (T increases with each of them), and each rounds to
+// nearest within 2^-24 relative, so the ~12 roundings leave the result at most 12 * 2^-24
+// below the exact T; multiplying by (1 + 2^-18) and stepping one ulp up covers that, the
+// 2^-38 and 2^-30 margins above, and v_sqrt_f32's error (< 1 ulp).
+__device__ __forceinline__ float f64p_threshold32(float amin, float m) {
+  const float M = m * (1.0f + 0x1p-20f);
+  const float al = 0x1p-17f, be = 0x1p-19f * M, g0 = 0x1p-38f * (M * M) + 0x1p-100f;
+  const float X = (be + __builtin_sqrtf(be * be + (4.0f - 0x1p-15f) * (g0 + amin))) *
+                  (1.0f / (2.0f - 0x1p-16f));
+  const float V = X * X;
+  const float T = (V + al * V + be * __builtin_sqrtf(V) + g0) * (1.0f + 0x1p-18f);
+  return __uint_as_float(__float_as_uint(T) + 1u);
+}
+#ifndef IVC_F64P_T32
+#define IVC_F64P_T32 1
+#endif
+#ifndef IVC_F64P_PREFETCH
+#define IVC_F64P_PREFETCH 0
+#endif
+
 template <int SR>
 __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const double* __restrict__ ref,
                                                             const double* __restrict__ cur,
@@ -85,6 +106,32 @@ __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const d
   const int h = H / 8, w = W / 8;
   const int segs = (w + nbr - 1) / nbr;
   const int64_t rounds = nframes * h * segs;
+  constexpr int NWI = (WR * WC + FLT_WG - 1) / FLT_WG, NBI = (nbr * 64 + FLT_WG - 1) / FLT_WG;
+  // the round's window and blocks as float64, every load of the thread issued before the first
+  // use (one memory latency per round)
+  auto load_round = [&](int64_t rr, int tid, double (&wv)[NWI], double (&bv)[NBI]) {
+    const bool ex = rr < rounds;
+    const int64_t f = ex ? rr / ((int64_t)h * segs) : 0;
+    const int rem = ex ? (int)(rr - f * h * segs) : 0, by = rem / segs, bx0 = (rem - by * segs) * nbr;
+    const int nb = w - bx0 < nbr ? w - bx0 : nbr;
+    const double* rf = ref + f * (int64_t)H * W;
+    const double* cf = cur + f * (int64_t)H * W;
+    const int y0 = 8 * by - SR, x0 = 8 * bx0 - SR, wc = nb * 8 + 2 * SR;
+#pragma unroll
+    for (int j = 0; j < NWI; ++j) {
+      const int i = tid + j * FLT_WG;
+      const int xx = i / WR, yy = i - xx * WR, gy = y0 + yy, gx = x0 + xx;
+      wv[j] = (ex && i < WR * wc && gy >= 0 && gy < H && gx >= 0 && gx < W) ? rf[(int64_t)gy * W + gx] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < NBI; ++j) {
+      const int i = tid + j * FLT_WG;
+      const int b = i >> 6, u = (i >> 3) & 7, v = i & 7;
+      bv[j] = ex && i < nb * 64 ? cf[(int64_t)(8 * by + u) * W + 8 * (bx0 + b) + v] : 0.0;
+    }
+  };
+  double wv[NWI], bv[NBI];
+  if (IVC_F64P_PREFETCH) load_round(blockIdx.x, threadIdx.x, wv, bv);
   for (int64_t r = blockIdx.x; r < rounds; r += gridDim.x) {
     // (opaque per round: the thread's index constants are formed in the loop instead of being
     // hoisted out of it, where they stay live — and spill — through the search)
@@ -96,7 +143,7 @@ __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const d
     const int nb = w - bx0 < nbr ? w - bx0 : nbr;
     const double* rf = ref + f * (int64_t)H * W;
     const double* cf = cur + f * (int64_t)H * W;
-    const int y0 = 8 * by - SR, x0 = 8 * bx0 - SR, wc = nb * 8 + 2 * SR;
+    const int wc = nb * 8 + 2 * SR;
     lds_barrier();                                  // the previous round's LDS reads are done
     if (tid == 0) {
       nsurv = 0;
@@ -111,23 +158,9 @@ __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const d
     }
     // stage the window (column-major float32, zeros outside the frame) and the blocks, checking
     // the bound's assumptions and taking max |x| on the way
-    // (every load of the thread issued before the first use: one memory latency per round)
     bool badl = false;
     float mwl = 0.f, mbl = 0.f;
-    constexpr int NWI = (WR * WC + FLT_WG - 1) / FLT_WG, NBI = (nbr * 64 + FLT_WG - 1) / FLT_WG;
-    double wv[NWI], bv[NBI];
-#pragma unroll
-    for (int j = 0; j < NWI; ++j) {
-      const int i = tid + j * FLT_WG;
-      const int xx = i / WR, yy = i - xx * WR, gy = y0 + yy, gx = x0 + xx;
-      wv[j] = (i < WR * wc && gy >= 0 && gy < H && gx >= 0 && gx < W) ? rf[(int64_t)gy * W + gx] : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < NBI; ++j) {
-      const int i = tid + j * FLT_WG;
-      const int b = i >> 6, u = (i >> 3) & 7, v = i & 7;
-      bv[j] = i < nb * 64 ? cf[(int64_t)(8 * by + u) * W + 8 * (bx0 + b) + v] : 0.0;
-    }
+    if (!IVC_F64P_PREFETCH) load_round(r, tid, wv, bv);
 #pragma unroll
     for (int j = 0; j < NWI; ++j) {
       const int i = tid + j * FLT_WG;
@@ -148,6 +181,8 @@ __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const d
       mbl = fmaxf(mbl, fabsf(fx));
       if (i < nb * 64) cbT[b * 64 + v * 8 + u] = fx;
     }
+    // (IVC_F64P_PREFETCH: the next round's loads fly during this round's search)
+    if (IVC_F64P_PREFETCH) load_round(r + gridDim.x, tid, wv, bv);
     lds_barrier();                                  // (the resets above are visible)
     if (badl) atomicOr(&bad, 1u);
     atomicMax(&mw, __float_as_uint(mwl));
@@ -198,8 +233,10 @@ __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const d
     }
     lds_barrier();
     if (bad == 0u && col) {
-      const float t = f64p_threshold(__uint_as_float(amin[sb]),
-                                     __uint_as_float(mw) + __uint_as_float(mb));
+      const float t = IVC_F64P_T32 ? f64p_threshold32(__uint_as_float(amin[sb]),
+                                                      __uint_as_float(mw) + __uint_as_float(mb))
+                                   : f64p_threshold(__uint_as_float(amin[sb]),
+                                                    __uint_as_float(mw) + __uint_as_float(mb));
 #pragma unroll
       for (int k = 0; k < n; ++k)
         if (k >= ky0 && k < ky1 && acc[k] <= t) {
