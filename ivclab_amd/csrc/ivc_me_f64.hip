@@ -83,6 +83,9 @@ __device__ __forceinline__ float f64p_threshold32(float amin, float m) {
 #ifndef IVC_F64P_T32
 #define IVC_F64P_T32 1
 #endif
+#ifndef IVC_F64P_MASK
+#define IVC_F64P_MASK 1
+#endif
 #ifndef IVC_F64P_PREFETCH
 #define IVC_F64P_PREFETCH 0
 #endif
@@ -194,6 +197,7 @@ __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const d
     float acc[n];
 #pragma unroll
     for (int k = 0; k < n; ++k) acc[k] = 0.f;
+    float m = __builtin_inff();                     // the lane's least A over its valid dy
     if (col) {
       const float* cb = cbT + sb * 64;
       const float* wcol = winT + (sb * 8 + se) * P;
@@ -206,26 +210,30 @@ __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const d
           const float4 q = *reinterpret_cast<const float4*>(cb + v * 8 + u);
           cv[u] = q.x; cv[u + 1] = q.y; cv[u + 2] = q.z; cv[u + 3] = q.w;
         }
+        // the next group of 4 rows is read one group ahead (its LDS latency under this group's
+        // 64 operations); the 8 differences of a row are formed before their 8 FMAs
+        float4 qn = *reinterpret_cast<const float4*>(wcol + v * P);
 #pragma unroll
         for (int r4 = 0; r4 < WR; r4 += 4) {
-          const float4 q = *reinterpret_cast<const float4*>(wcol + v * P + r4);
+          const float4 q = qn;
+          if (r4 + 4 < WR) qn = *reinterpret_cast<const float4*>(wcol + v * P + r4 + 4);
+          // (no later LDS read moves above this point: the compiler would hoist the whole
+          // column's reads and spill)
+          __asm__ volatile("" ::: "memory");
           const float wq[4] = {q.x, q.y, q.z, q.w};
 #pragma unroll
-          for (int t = 0; t < 4; ++t)
+          for (int t = 0; t < 4; ++t) {
+            float d[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) d[u] = cv[u] - wq[t];
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
               const int k = r4 + t - u;
-              if (k >= 0 && k < n) {
-                const float d = cv[u] - wq[t];
-                acc[k] = __builtin_fmaf(d, d, acc[k]);
-              }
+              if (k >= 0 && k < n) acc[k] = __builtin_fmaf(d[u], d[u], acc[k]);
             }
-          // (no LDS read moves above this point: the compiler would hoist the whole column's
-          // reads and spill)
-          __asm__ volatile("" ::: "memory");
+          }
         }
       }
-      float m = __builtin_inff();
 #pragma unroll
       for (int k = 0; k < n; ++k)
         if (k >= ky0 && k < ky1) m = fminf(m, acc[k]);
@@ -237,12 +245,29 @@ __global__ __launch_bounds__(FLT_WG, IVC_F64P_WAVES) void me_f64p_kernel(const d
                                                       __uint_as_float(mw) + __uint_as_float(mb))
                                    : f64p_threshold(__uint_as_float(amin[sb]),
                                                     __uint_as_float(mw) + __uint_as_float(mb));
+#if IVC_F64P_MASK
+      // only lanes whose least A is within T have survivors: their dy as a bit mask, then one
+      // append per set bit (usually one)
+      if (m <= t) {
+        uint64_t mk = 0;
+#pragma unroll
+        for (int k = 0; k < n; ++k)
+          mk |= (uint64_t)(k >= ky0 && k < ky1 && acc[k] <= t) << k;
+        while (mk) {
+          const int k = __builtin_ctzll(mk);
+          mk &= mk - 1;
+          const uint32_t slot = atomicAdd(&nsurv, 1u);
+          if (slot < (uint32_t)F64P_CAP) ent[slot] = ((uint32_t)sb << 16) | (uint32_t)(k * n + se);
+        }
+      }
+#else
 #pragma unroll
       for (int k = 0; k < n; ++k)
         if (k >= ky0 && k < ky1 && acc[k] <= t) {
           const uint32_t slot = atomicAdd(&nsurv, 1u);
           if (slot < (uint32_t)F64P_CAP) ent[slot] = ((uint32_t)sb << 16) | (uint32_t)(k * n + se);
         }
+#endif
     }
     lds_barrier();
     const uint32_t ns = nsurv;
