@@ -70,7 +70,11 @@ enum ivc_tuning_key {
      1 = without the float32 bound phase (every candidate in float64), 2 = the bound phase
      defers every round to the float64 search (exercises the deferral path); 0 = pruned */
   IVC_TUNE_F64_ME = 5,
-  IVC_TUNE_COUNT = 6
+  /* 1 = the per-block calls (one (8, 8) DCT, one (C, 8, 8) quantise / dequantise through the
+     host-buffer entry points) launch a kernel each instead of using the resident tiny-call
+     server; 0 = the server */
+  IVC_TUNE_TINY_SERVER = 6,
+  IVC_TUNE_COUNT = 7
 };
 int ivc_set_tuning(int key, int value);
 /* the current override of `key` (0: none), or IVC_E_ARG for an unknown key */

@@ -284,7 +284,7 @@ def empty_like(a) -> np.ndarray:
 
 # ivc_set_tuning keys (include/ivc.h enum ivc_tuning_key)
 TUNE = {"zr_chunks": 0, "sym_chunks": 1, "s2i_chunks": 2, "inter_chunks": 3, "s2i_no_fallback": 4,
-        "f64_me": 5}
+        "f64_me": 5, "tiny_server": 6}
 
 
 def set_tuning(name: str, value: int) -> int:

@@ -15,6 +15,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <cstdlib>
 #include <vector>
 
 #include "ivc_internal.h"
@@ -175,6 +176,15 @@ struct DevCtx {
   double* tiny_tab = nullptr;               // device copy of the last quantiser table of a tiny call
   QTab tiny_tab_host;                       // its values
   bool tiny_tab_valid = false;
+  // the resident tiny-call server (tiny_server_kernel): its mailbox (coherent page-locked
+  // host memory), its own stream, the generation of the last launch and the request sequence
+  SrvBox* srv = nullptr;
+  hipStream_t srv_stream = nullptr;
+  int srv_state = 0;                        // 0 untried, 1 ready, -1 unavailable
+  bool srv_launched = false;
+  uint32_t srv_gen = 0, srv_seq = 0, srv_tab_ver = 0;
+  QTab srv_tab;
+  bool srv_tab_valid = false;
   void* slot[kSlots] = {};
   size_t cap[kSlots] = {};
   void* pin[kPinSlots] = {};
@@ -249,6 +259,19 @@ bool pinned_ready(DevCtx* c) {
     (void)hipGetLastError();
   }
   return c->pin_state == 1;
+}
+
+// at process exit, every resident tiny-call server is asked to leave (it would leave by itself
+// after its idle time in any case)
+void stop_servers() {
+  for (int d = 0; d < kMaxDev; ++d) {
+    DevCtx& c = g_ctx[d];
+    if (c.srv_state == 1 && c.srv_launched && c.srv) __atomic_store_n(&c.srv->h.req, SRV_STOP, __ATOMIC_RELEASE);
+  }
+}
+void register_server_exit() {
+  static std::once_flag once;
+  std::call_once(once, [] { std::atexit(stop_servers); });
 }
 
 int current_device(int* dev) {
@@ -457,6 +480,100 @@ struct Staging {
       if (e != hipSuccess) { status = fail_hip(e, "hipStreamSynchronize"); return true; }
     }
     if (OB) memcpy(dst, to, OB);
+    return true;
+  }
+  // A per-block call through the resident tiny-call server (ivc_kernels.hip tiny_server_kernel):
+  // the request is written into the mailbox, the server's wave answers it, the output is copied
+  // out — no kernel launch per call (tools/ubench/mailbox.hip: 4.3 us per round trip against
+  // ~6.4 us for a launch and its completion).  The server leaves after kSrvIdle ticks without a
+  // request (so a device-wide synchronisation waits at most that long after the last call) or
+  // kSrvLife in all, and is relaunched on the next call.  Returns false, nothing done, when the
+  // server is off (ivc_set_tuning(IVC_TUNE_TINY_SERVER, 1)), unavailable or the call too large.
+  static constexpr uint64_t kSrvIdle = 50000, kSrvLife = 100000000;     // 0.5 ms, 1 s (100 MHz)
+  bool server(uint32_t op, int sdt, int ddt, int inverse, int ortho, double fct, int C, const QTab* t,
+              const void* src, size_t IB, void* dst, size_t OB) {
+    if (status || tuning(IVC_TUNE_TINY_SERVER) == 1 || IB > (size_t)SRV_IO || OB > (size_t)SRV_IO)
+      return false;
+    DevCtx* c = ctx;
+    if (c->srv_state == 0) {
+      c->srv_state = -1;
+      if (hipHostMalloc((void**)&c->srv, sizeof(SrvBox), hipHostMallocCoherent | hipHostMallocMapped) ==
+              hipSuccess &&
+          hipStreamCreateWithFlags(&c->srv_stream, hipStreamNonBlocking) == hipSuccess) {
+        memset((void*)c->srv, 0, sizeof(SrvBox));
+        c->srv_state = 1;
+        register_server_exit();
+      }
+      (void)hipGetLastError();
+    }
+    if (c->srv_state != 1) return false;
+    SrvBox* b = c->srv;
+    auto relaunch = [&]() -> bool {
+      if (++c->srv_gen == 0) c->srv_gen = 1;
+      if (launch_tiny_server(b, c->srv_gen, kSrvIdle, kSrvLife, c->srv_stream) != hipSuccess) {
+        (void)hipGetLastError();
+        c->srv_state = -1;
+        c->srv_launched = false;
+        return false;
+      }
+      c->srv_launched = true;
+      return true;
+    };
+    auto gone = [&]() { return __atomic_load_n(&b->exited, __ATOMIC_ACQUIRE) == c->srv_gen; };
+    if ((!c->srv_launched || gone()) && !relaunch()) return false;
+    if (t && (!c->srv_tab_valid || memcmp(c->srv_tab.q, t->q, sizeof(QTab)) != 0)) {
+      memcpy(b->tab, t->q, sizeof(QTab));
+      if (++c->srv_tab_ver == 0) c->srv_tab_ver = 1;
+      c->srv_tab = *t;
+      c->srv_tab_valid = true;
+    }
+    uint32_t seq = ++c->srv_seq;
+    if (seq == 0 || seq == SRV_STOP) seq = c->srv_seq = 1;
+    // header and input, then the checksum the server verifies its one-read snapshot against
+    // (over the header words with the new sequence and the whole input area), then the sequence
+    SrvHdr hd;
+    memset(&hd, 0, sizeof(hd));
+    hd.req = seq;
+    hd.op = op;
+    hd.src_dtype = (uint32_t)sdt;
+    hd.dst_dtype = (uint32_t)ddt;
+    hd.inverse = (uint32_t)inverse;
+    hd.ortho = (uint32_t)ortho;
+    hd.C = (uint32_t)C;
+    hd.tab_ver = c->srv_tab_ver;
+    hd.nin = (uint32_t)IB;
+    hd.nout = (uint32_t)OB;
+    hd.fct = fct;
+    memcpy((void*)b->in, src, IB);
+    uint64_t hq[8];
+    memcpy(hq, &hd, sizeof(hq));
+    uint64_t sum = 0;
+    for (uint32_t k = 0; k < 6; ++k) sum += srv_mix(hq[k], k);
+    const volatile uint64_t* inw = b->in;
+    for (uint32_t k = 0; k < (uint32_t)SRV_IO / 8; ++k) sum += srv_mix(inw[k], 6u + k);
+    volatile uint32_t* hv = reinterpret_cast<volatile uint32_t*>(&b->h);
+    const uint32_t* hs = reinterpret_cast<const uint32_t*>(&hd);
+    for (int k = 1; k < 12; ++k) hv[k] = hs[k];                     // words after req
+    __atomic_store_n(&b->h.sum, sum, __ATOMIC_RELEASE);
+    __atomic_store_n(&b->h.req, seq, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+      if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) break;
+      __builtin_ia32_pause();
+      if ((i & 255u) == 0) {
+        // the server may have left between our check and the request: a new one serves it
+        if (gone() && !relaunch()) {
+          status = fail(IVC_E_DEVICE, "tiny-call server could not be relaunched");
+          return true;
+        }
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+          c->srv_state = -1;                 // never again in this process
+          status = fail(IVC_E_DEVICE, "tiny-call server did not answer");
+          return true;
+        }
+      }
+    }
+    memcpy(dst, (const void*)b->out, OB);
     return true;
   }
   int sync() {
@@ -695,6 +812,15 @@ int ivc_dct8x8(const void* src, int src_dtype, int64_t nblk, void* dst, int dst_
   TRY(st.open());
   const size_t ib = (size_t)nblk * 64 * dtype_size(src_dtype);
   const size_t ob = (size_t)nblk * 64 * dtype_size(dst_dtype);
+  if (nblk == 1 && (dst_dtype == IVC_F64 || src_dtype == IVC_F32) &&
+      !(dst_dtype == IVC_F64 && src_dtype == IVC_F32)) {
+    // scipy's normalisation (as launch_dct8x8): inverse transforms use 2 - norm
+    const int inorm = inverse ? 2 - norm : norm;
+    const double fct = inorm == 0 ? 1.0 : (inorm == 1 ? 0.25 : 0.0625);
+    if (st.server(SRV_DCT, src_dtype, dst_dtype, inverse, norm == IVC_NORM_ORTHO, fct, 0, nullptr, src, ib,
+                  dst, ob))
+      return st.status;
+  }
   if (st.tiny(src, ib, dst, ob, "dct8x8", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
         return launch_dct8x8(i, src_dtype, nblk, o, dst_dtype, inverse, norm, s, d);
       }))
@@ -765,6 +891,10 @@ int ivc_quantize(const void* src, int src_dtype, int64_t nblk, int C, const doub
   Staging st;
   TRY(st.open());
   const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
+  // float32 arithmetic only for float32 or <= 16-bit integer inputs (as launch_quant_common)
+  if (nblk == 1 && (calc_dtype == IVC_F64 || dtype_size(src_dtype) <= 2 || src_dtype == IVC_F32) &&
+      st.server(SRV_QUANT, src_dtype, calc_dtype, 0, 0, 0.0, C, &t, src, ib, dst, ob))
+    return st.status;
   if (st.tiny(src, ib, dst, ob, "quantize", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
         return launch_quantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s, d,
                                tiny_table(st.ctx, t));
@@ -803,6 +933,10 @@ int ivc_dequantize(const void* src, int src_dtype, int64_t nblk, int C, const do
   Staging st;
   TRY(st.open());
   const size_t ib = (size_t)nblk * C * 64 * dtype_size(src_dtype), ob = (size_t)nblk * 192 * 4;
+  // float32 arithmetic only for float32 or <= 16-bit integer inputs (as launch_quant_common)
+  if (nblk == 1 && (calc_dtype == IVC_F64 || dtype_size(src_dtype) <= 2 || src_dtype == IVC_F32) &&
+      st.server(SRV_DEQUANT, src_dtype, calc_dtype, 0, 0, 0.0, C, &t, src, ib, dst, ob))
+    return st.status;
   if (st.tiny(src, ib, dst, ob, "dequantize", [&](const void* i, void* o, hipStream_t s, const TinyDone* d) {
         return launch_dequantize(i, src_dtype, nblk, C, t, calc_dtype, (int32_t*)o, s, d,
                                  tiny_table(st.ctx, t));

@@ -283,4 +283,42 @@ template <typename T, int SR> struct FltGeom {
 bool launch_me_f64p(int sr, const double* ref, const double* cur, int64_t nf, int H, int W,
                     int64_t* mv, uint32_t* defer, int defer_all, hipStream_t s);
 
+
+// ---- tiny-call server (ivc_kernels.hip tiny_server_kernel, ivc_capi.hip server_call) ----
+// A resident one-wave kernel serving the reference's per-block calls (one (8, 8) DCT, one
+// (C, 8, 8) quantise / dequantise) through a mailbox in coherent page-locked host memory,
+// instead of one kernel launch per call.  Host -> device fields first, device -> host after;
+// each group on its own 128-byte lines.
+enum { SRV_DCT = 1, SRV_QUANT = 2, SRV_DEQUANT = 3 };
+constexpr uint32_t SRV_STOP = 0xffffffffu;
+constexpr int SRV_IO = 1536;                     // bytes of input and of output at most
+// A request is read in one go: the header line and the whole input area, every poll (no
+// dependent second read).  The host writes the header and the input, then a 64-bit checksum
+// of them and of the sequence (srv_sum), then the sequence; the server acts on a poll only if
+// the sequence is new and the checksum matches what it read, and polls again otherwise (a
+// snapshot taken while the host was still writing).
+struct SrvHdr {
+  uint32_t req;                                  // request sequence (host writes last)
+  uint32_t op, src_dtype, dst_dtype, inverse, ortho, C, tab_ver, nin, nout;
+  double fct;
+  uint64_t sum;                                  // srv_sum of words 0..5 and the input
+  uint64_t pad;
+};
+static_assert(sizeof(SrvHdr) == 64, "one 64-byte header");
+struct alignas(128) SrvBox {
+  SrvHdr h;
+  uint32_t pad0[16];
+  alignas(128) uint64_t in[SRV_IO / 8];
+  double tab[192];                               // the quantiser table of version tab_ver
+  alignas(128) uint32_t done;                    // last request served (device writes last)
+  uint32_t exited;                               // generation of the server that left its loop
+  uint32_t pad3[30];
+  alignas(128) uint64_t out[SRV_IO / 8];
+};
+__host__ __device__ inline uint64_t srv_mix(uint64_t w, uint32_t k) {
+  return (w ^ ((uint64_t)(k + 1) * 0x9E3779B97F4A7C15ull)) * 0xD6E8FEB86659FD93ull;
+}
+hipError_t launch_tiny_server(SrvBox* box, uint32_t gen, uint64_t idle_ticks, uint64_t life_ticks,
+                              hipStream_t s);
+
 }  // namespace ivc

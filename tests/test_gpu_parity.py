@@ -116,6 +116,46 @@ def test_tiny_calls_zero_copy():
         assert_bits(z, O.zigzag_scan(blk.astype(np.int32)), "zigzag_scan")
 
 
+@pytest.mark.parametrize("server", [0, 1])
+def test_tiny_server_and_launch_paths(server, tune):
+    """The per-block calls through the resident tiny-call server (server 0, the default) and
+    through one kernel launch each (server 1 = off): every DCT source dtype (float32 -> float32,
+    the rest -> float64), forward and inverse, every norm; quantise and dequantise of (1, 8, 8)
+    and (3, 8, 8) stacks of several dtypes in float64 and float32 arithmetic, the table changed
+    between calls (the server's cached copy must follow); the server left idle long enough to
+    exit and relaunched; a device-wide synchronisation right after a call (the resident wave
+    leaves within its idle time)."""
+    import time
+    import torch
+    tune("tiny_server", server)
+    rng = np.random.default_rng(900 + server)
+    for norm in ("ortho", "backward", "forward"):
+        dct = DiscreteCosineTransform(norm=norm)
+        for dt in (np.float64, np.float32, np.uint8, np.int16, np.int32, np.int64):
+            x = (rng.normal(0, 60, (8, 8)) if dt in (np.float64, np.float32)
+                 else rng.integers(0, 200, (8, 8))).astype(dt)
+            assert_bits(dct.transform(x), O.dct_transform(x, norm=norm), f"dct {norm} {dt.__name__}")
+            assert_bits(dct.inverse_transform(x), O.dct_inverse(x, norm=norm), f"idct {norm} {dt.__name__}")
+    for scale in (1.0, 0.5, 0.15):
+        pq = PatchQuant(scale)
+        for C in (1, 3):
+            for dt in (np.float64, np.float32, np.int16, np.int32):
+                x = (rng.normal(0, 80, (C, 8, 8)) if dt in (np.float64, np.float32)
+                     else rng.integers(-300, 300, (C, 8, 8))).astype(dt)
+                assert_bits(pq.quantize(x), O.quantize(x, scale), f"quantize s={scale} C={C} {dt.__name__}")
+                assert_bits(pq.dequantize(x.astype(np.int32)), O.dequantize(x.astype(np.int32), scale),
+                            f"dequantize s={scale} C={C}")
+    blk = rng.normal(0, 50, (8, 8))
+    time.sleep(0.01)                                     # past the server's idle time: it leaves
+    assert_bits(DCT.transform(blk), O.dct_transform(blk), "after idle exit")
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t0 < 0.1
+    for _ in range(200):                                 # back to back
+        blk = rng.normal(0, 50, (8, 8))
+        assert_bits(DCT.transform(blk), O.dct_transform(blk), "loop")
+
+
 def test_tiny_inline_capacity_mismatch():
     """Inputs of 513-1536 B through the tiny path (above the one-block DCT launcher's 512 B
     argument capacity, within the general one's): several blocks per DCT call, float64 stacks

@@ -18,4 +18,8 @@ stk = rng.normal(0, 50, (3, 8, 8))
 dct, pq = DiscreteCosineTransform(), PatchQuant(1.0)
 assert np.array_equal(dct.transform(blk), O.dct_transform(blk))
 assert np.array_equal(pq.quantize(stk), O.quantize(stk, 1.0))
-print(json.dumps(bench.small_call_us(dct, pq, O, blk, stk)))
+from ivclab_amd import _native as N  # noqa: E402
+for srv in (0, 1, 0):
+    prev = N.set_tuning("tiny_server", srv)
+    print(json.dumps(dict(bench.small_call_us(dct, pq, O, blk, stk), tiny_server=srv == 0)))
+    N.set_tuning("tiny_server", prev)

@@ -207,5 +207,24 @@ int main() {
   run("ivc_quantize f64 (3,8,8) host call", [&](int) {
     if (ivc_quantize(q3, IVC_F64, 1, 3, tb, IVC_F64, qo) != 0) printf("err %s\n", ivc_last_error());
   });
+  double bd[64];
+  for (int i = 0; i < 64; ++i) bd[i] = i * 1.37 - 40;
+  for (int srv = 0; srv < 2; ++srv) {
+    ivc_set_tuning(IVC_TUNE_TINY_SERVER, srv);
+    printf("-- tiny-call server %s\n", srv ? "off (one launch per call)" : "on");
+    run("  ivc_dct8x8 u8 (8,8) -> f64", [&](int) {
+      if (ivc_dct8x8(blk, IVC_U8, 1, out, IVC_F64, 0, IVC_NORM_ORTHO) != 0) printf("err %s\n", ivc_last_error());
+    });
+    run("  ivc_dct8x8 f64 (8,8) -> f64", [&](int) {
+      if (ivc_dct8x8(bd, IVC_F64, 1, out, IVC_F64, 0, IVC_NORM_ORTHO) != 0) printf("err %s\n", ivc_last_error());
+    });
+    run("  ivc_quantize f64 (3,8,8)", [&](int) {
+      if (ivc_quantize(q3, IVC_F64, 1, 3, tb, IVC_F64, qo) != 0) printf("err %s\n", ivc_last_error());
+    });
+    run("  ivc_quantize f64 (1,8,8)", [&](int) {
+      if (ivc_quantize(q3, IVC_F64, 1, 1, tb, IVC_F64, qo) != 0) printf("err %s\n", ivc_last_error());
+    });
+  }
+  ivc_set_tuning(IVC_TUNE_TINY_SERVER, 0);
   return 0;
 }
