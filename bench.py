@@ -1052,10 +1052,13 @@ def small_call_us(dct, pq, O, blk, stk, reps=400, warm=50):
         med, mean = stats(fn)
         r[key + "_us"] = med
         r[key + "_mean_us"] = mean
-    r["note"] = ("median per call (mean beside it); one launch per call: the input rides in the "
-                 "kernel arguments, a one-wave kernel writes the result into page-locked memory and "
-                 "a completion word the host spins on (DESIGN.md §1); NumPy is faster per call at "
-                 "this size")
+    from ivclab_amd import _native as N
+    r["tiny_server"] = N.lib().ivc_tuning(N.TUNE["tiny_server"]) != 1
+    r["vs_numpy"] = {"transform": round(r["transform_8x8_numpy_us"] / r["transform_8x8_us"], 2),
+                     "quantize": round(r["quantize_3x8x8_numpy_us"] / r["quantize_3x8x8_us"], 2)}
+    r["note"] = ("median per call (mean beside it); vs_numpy = NumPy time / ours.  A resident "
+                 "one-wave server polls a page-locked request block and answers in page-locked "
+                 "memory (DESIGN.md §1); with it off, one launch per call")
     return r
 
 

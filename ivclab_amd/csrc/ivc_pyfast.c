@@ -141,11 +141,107 @@ static PyObject* quant(PyObject* self, PyObject* const* args, Py_ssize_t nargs) 
   return (PyObject*)out;
 }
 
+/* an (8, 8) table operand: an exact, C-contiguous, aligned, host-order ndarray of float32
+ * (*kind = 1), float64 (2) or int64 (3) */
+static const void* table_block(PyObject* o, int* kind) {
+  if (Py_TYPE(o) != &PyArray_Type) return NULL;
+  PyArrayObject* a = (PyArrayObject*)o;
+  if (PyArray_NDIM(a) != 2 || PyArray_DIMS(a)[0] != 8 || PyArray_DIMS(a)[1] != 8) return NULL;
+  if (PyArray_ISBYTESWAPPED(a) || !PyArray_IS_C_CONTIGUOUS(a) || !PyArray_ISALIGNED(a)) return NULL;
+  const int t = PyArray_DESCR(a)->type_num;
+  if (t == NPY_FLOAT32) {
+    *kind = 1;
+  } else if (t == NPY_FLOAT64) {
+    *kind = 2;
+  } else if (PyArray_ITEMSIZE(a) == 8 && (t == NPY_LONG || t == NPY_LONGLONG)) {
+    *kind = 3;
+  } else {
+    return NULL;
+  }
+  return PyArray_DATA(a);
+}
+
+static double table_value(const void* p, int kind, int i) {
+  return kind == 1 ? (double)((const float*)p)[i]
+                   : kind == 2 ? ((const double*)p)[i] : (double)((const int64_t*)p)[i];
+}
+
+/* quant_lc(dequantize, x, luminance, chrominance, scale) -> out | status | None: the table
+ * formed here as PatchQuant.get_quantization_table forms it (patchquant.py:39-42:
+ * stack([lum, chrom, chrom]) * scale), under NumPy 2's promotion rules, when that is a float32
+ * or float64 table.  The stack is float32 when both tables are, int64 when both are int64,
+ * float64 otherwise.  A Python float or int scale is weak (it takes the stack's type: float32
+ * multiplies in float32, an int64 stack times an int stays int64 and is declined); a float64
+ * scalar is strong (the product is float64).  Ints are taken up to 2^24 (float32) / 2^53
+ * (float64) in magnitude, where the conversion is exact.  NumPy converts each entry to the
+ * result type and multiplies element by element, so every entry is the same correctly rounded
+ * value as here.  None for anything else (other scale types, other table dtypes or layouts). */
+static PyObject* quant_lc(PyObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 5 || !g_quant || !g_dequant) Py_RETURN_NONE;
+  int lk = 0, ck = 0;
+  const void* lum = table_block(args[2], &lk);
+  const void* chrom = table_block(args[3], &ck);
+  if (!lum || !chrom) Py_RETURN_NONE;
+  const int stack = lk == ck ? lk : 2;                 /* 1 float32, 2 float64, 3 int64 */
+  PyObject* so = args[4];
+  double sc;
+  int f32;                                             /* the table's type: float32 or float64 */
+  if (PyFloat_CheckExact(so)) {
+    sc = PyFloat_AS_DOUBLE(so);
+    f32 = stack == 1;
+  } else if (PyFloat_Check(so) && PyArray_IsScalar(so, Double)) {
+    sc = PyFloat_AS_DOUBLE(so);
+    f32 = 0;
+  } else if (PyLong_CheckExact(so) && stack != 3) {
+    int ovf = 0;
+    const long long v = PyLong_AsLongLongAndOverflow(so, &ovf);
+    const long long lim = stack == 1 ? (1LL << 24) : (1LL << 53);
+    if (ovf || v > lim || v < -lim) Py_RETURN_NONE;
+    sc = (double)v;
+    f32 = stack == 1;
+  } else {
+    Py_RETURN_NONE;
+  }
+  double tab[192];
+  if (f32) {
+    const volatile float s32 = (float)sc;
+    for (int i = 0; i < 64; ++i) {
+      const volatile float pl = ((const float*)lum)[i] * s32;
+      const volatile float pc = ((const float*)chrom)[i] * s32;
+      tab[i] = pl;
+      tab[64 + i] = tab[128 + i] = pc;
+    }
+  } else {
+    for (int i = 0; i < 64; ++i) {
+      tab[i] = table_value(lum, lk, i) * sc;
+      tab[64 + i] = tab[128 + i] = table_value(chrom, ck, i) * sc;
+    }
+  }
+  PyObject* a4[4];
+  a4[0] = args[0];
+  a4[1] = args[1];
+  PyObject* addr = PyLong_FromUnsignedLongLong((unsigned long long)(uintptr_t)tab);
+  PyObject* code = PyLong_FromLong(f32 ? 9 : 10);
+  if (!addr || !code) {
+    Py_XDECREF(addr);
+    Py_XDECREF(code);
+    return NULL;
+  }
+  a4[2] = addr;
+  a4[3] = code;
+  PyObject* r = quant(self, a4, 4);
+  Py_DECREF(addr);
+  Py_DECREF(code);
+  return r;
+}
+
 static PyMethodDef methods[] = {
     {"set_entry_points", set_entry_points, METH_VARARGS, "the C-ABI entry points"},
     {"dct8x8", (PyCFunction)(void (*)(void))dct8x8, METH_FASTCALL, "one-step DCT of small arrays"},
     {"quant", (PyCFunction)(void (*)(void))quant, METH_FASTCALL,
      "one-step (de)quantisation of small arrays"},
+    {"quant_lc", (PyCFunction)(void (*)(void))quant_lc, METH_FASTCALL,
+     "one-step (de)quantisation with the table formed from luminance, chrominance and scale"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_ivcfast", NULL, -1, methods};

@@ -117,8 +117,15 @@ class PatchQuant:
         # a C-contiguous array of a kernel dtype whose block axes need no broadcasting; the
         # per-(dtype, shape) launch arguments are cached
         if type(x) is np.ndarray and x.size <= 12288:
-            table, targ, tptr = self._table_args()
             F = N.fast()
+            if F is not None and type(self) is PatchQuant:     # the table formed in the C step
+                r = F.quant_lc(entry == "ivc_dequantize", x, self.luminance, self.chrominance,
+                               self.quantization_scale)
+                if r is not None:
+                    if type(r) is int:
+                        N.check(r, what)
+                    return r
+            table, targ, tptr = self._table_args()
             tdt = table.dtype
             if F is not None and tptr is not None and (tdt is _F64 or tdt is _F32):   # one C step
                 r = F.quant(entry == "ivc_dequantize", x, tptr, 10 if tdt is _F64 else 9)

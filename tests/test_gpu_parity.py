@@ -219,6 +219,22 @@ def test_tiny_call_fast_paths_match_general_path():
     q = pq2.quantize(stk)
     assert_bits(pq2.dequantize(q), (q * pq2.get_quantization_table()[None, None]).astype(np.int32),
                 "dequantize")
+    # the table formed in the C step under NumPy's promotion (ivc_pyfast.c quant_lc) and the
+    # tables it declines, each against NumPy's own table
+    u8 = rng.integers(0, 256, (3, 8, 8)).astype(np.uint8)
+    lum64 = rng.uniform(1, 90, (8, 8))
+    for lum, chrom, sc, xin in [(None, None, 0.3, u8), (None, None, 3, stk.astype(np.float32)),
+                                (lum64, None, 2, stk), (lum64, lum64, np.float64(0.7), u8),
+                                (lum64.astype(np.int64), None, 0.5, stk),
+                                (lum64.astype(np.int64) + 1, lum64.astype(np.int64) + 2, 1.5, u8),
+                                (lum64.astype(np.int32) + 1, None, 1.0, stk),     # declined
+                                (None, None, np.float32(0.8), stk.astype(np.float32))]:  # declined
+        p = PatchQuant(sc, lum, chrom)
+        t = p.get_quantization_table()
+        want = np.round(xin / t[None, None]).astype(np.int32)
+        assert_bits(p.quantize(xin), want, f"table {t.dtype} scale {sc!r} input {xin.dtype}")
+        q = p.quantize(xin)
+        assert_bits(p.dequantize(q), (q * t[None, None]).astype(np.int32), f"dequantize {t.dtype}")
 
 
 def test_dct_golden(golden):
