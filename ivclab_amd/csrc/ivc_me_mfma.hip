@@ -38,6 +38,16 @@
 
 #include <type_traits>
 
+#ifndef IVC_ME_EPRE
+#define IVC_ME_EPRE 4  // window-energy rows read this many rows ahead (0: as the compiler places them;
+                       // r06 A/Bs: profiles/r06w_ab_me_energy.log, r06x_ab_me_energy_base.log)
+#endif
+#ifndef IVC_ME_EBASE
+#define IVC_ME_EBASE 1 // (with EPRE) the rows' LDS addresses from one base per 8 rows
+#endif
+#ifndef IVC_ME_EFAST
+#define IVC_ME_EFAST 1 // interior tiles form the energies without the frame checks
+#endif
 #ifndef IVC_ME_ABL
 #define IVC_ME_ABL 0   // tools/ab timing builds only (results wrong; profiles/r06f_ab_me_ablation.log):
                        // 1 no energies, 2 keys of one quad only, 4 no staging writes, 8 no search
@@ -318,13 +328,46 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
         const int xb = 8 * bx0 - SR, yb = 8 * by - SR;
         const bool xok = xb + u >= 0 && xb + u + 8 <= W;
         const int rlo = half ? 20 : 0, rhi = half ? NR : 20;     // offsets of this thread
-        auto energy = [&](auto hf) {
+        auto energy = [&](auto hf, auto edge) {
           constexpr int RL = decltype(hf)::value ? 20 : 0, RH = decltype(hf)::value ? NR : 20;
-          int P[RH + 7 - RL + 1];
+          constexpr bool EDGE = decltype(edge)::value;
+          constexpr int NROW = RH + 7 - RL;
+          int P[NROW + 1];
           int pr = 0;
+#if IVC_ME_EPRE > 0
+          // the rows read IVC_ME_EPRE ahead (each read otherwise waits its whole LDS latency)
+          uint32_t b0[IVC_ME_EPRE], b1[IVC_ME_EPRE];
+#if IVC_ME_EBASE
+          // one opaque base per 8 rows, so each row's two dwords are one ds_read2 with constant
+          // offsets (the compiler otherwise forms every row's address with its own add)
+          int rb[(NROW + 7) / 8];
+#pragma unroll
+          for (int k = 0; k < (NROW + 7) / 8; ++k) {
+            rb[k] = (u & 3) * COPY + (u >> 2) + (RL + 8 * k) * PITCH;
+            asm volatile("" : "+v"(rb[k]));
+          }
+          auto rd = [&](int r, int dw) { return lds[rb[(r - RL) >> 3] + ((r - RL) & 7) * PITCH + dw]; };
+#else
+          auto rd = [&](int r, int dw) { return cw[r * PITCH + dw]; };
+#endif
+#pragma unroll
+          for (int k = 0; k < IVC_ME_EPRE; ++k) {
+            b0[k] = rd(RL + k, 0);
+            b1[k] = rd(RL + k, 1);
+          }
+#endif
 #pragma unroll
           for (int r = RL; r < RH + 7; ++r) {
+#if IVC_ME_EPRE > 0
+            const int w0 = (int)b0[(r - RL) % IVC_ME_EPRE], w1 = (int)b1[(r - RL) % IVC_ME_EPRE];
+            if (r + IVC_ME_EPRE < RH + 7) {
+              b0[(r - RL) % IVC_ME_EPRE] = rd(r + IVC_ME_EPRE, 0);
+              b1[(r - RL) % IVC_ME_EPRE] = rd(r + IVC_ME_EPRE, 1);
+            }
+            asm volatile("" ::: "memory");
+#else
             const int w0 = (int)cw[r * PITCH], w1 = (int)cw[r * PITCH + 1];
+#endif
             pr = __builtin_amdgcn_sdot4(w1, w1, __builtin_amdgcn_sdot4(w0, w0, pr, false), false);
             P[r - RL] = pr;
             if (r >= RL + 7) {
@@ -332,15 +375,29 @@ __global__ __launch_bounds__(256, 4) void me_mfma16x2_kernel(const uint8_t* __re
               const int t = (r - 8 >= RL ? P[r - 8 - RL] : 0) - pr;
               const int wv = R < 11 ? 0 : (R - 1) / 10;
               const int rank = (R - wave_r0(wv)) * NMT + (u >> 4);
-              const bool ok = xok && (unsigned)(yb + R) <= (unsigned)(H - 8);
-              lds[E_OFF + R * U + u] = (uint32_t)((ok ? (1 << 27) + 127 - rank : E_OUT) + 128 * t);
+              if (EDGE) {
+                const bool ok = xok && (unsigned)(yb + R) <= (unsigned)(H - 8);
+                lds[E_OFF + R * U + u] = (uint32_t)((ok ? (1 << 27) + 127 - rank : E_OUT) + 128 * t);
+              } else {
+                lds[E_OFF + R * U + u] = (uint32_t)((1 << 27) + 127 - rank + 128 * t);
+              }
             }
           }
         };
         (void)rlo;
         (void)rhi;
-        if (half) energy(std::true_type{});
-        else energy(std::false_type{});
+#if IVC_ME_EFAST
+        // a tile whose windows all lie inside the frame (workgroup-uniform) skips the checks
+        const bool inner = xb >= 0 && xb + U + 8 <= W && yb >= 0 && yb + NR + 7 <= H;
+        if (inner) {
+          if (half) energy(std::true_type{}, std::false_type{});
+          else energy(std::false_type{}, std::false_type{});
+        } else
+#endif
+        {
+          if (half) energy(std::true_type{}, std::true_type{});
+          else energy(std::false_type{}, std::true_type{});
+        }
       }
     }
     const mf_v4i bop = mf_v4i{L.bop.x ^ (int)0x80808080u, L.bop.y ^ (int)0x80808080u,
