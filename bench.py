@@ -634,7 +634,8 @@ def leg_luma_only(args, dist, rank, world, dev, table, frames, result, verify):
         "metric": "Mpixels/s: 4K intra DCT+quant, luma-table plane only (not the reference's 3-plane output), unpaced",
         "value": round(world * F * H * W * args.steps / wall / 1e6, 1), "unit": "Mpixels/s",
         "ms_per_step": round(wall / args.steps * 1e3, 3),
-        "roofline": {"bound": "hbm", "kernel": "fused_encode_kernel<u8,f64,C=1,OUT_LUMA>",
+        "roofline": {"bound": "issue (VALU; frac is against HBM), DESIGN.md 5",
+                     "kernel": "fused_encode_kernel<u8,f64,C=1,OUT_LUMA>",
                      "kernel_ms": round(ms, 4), "achieved": round(algo / (ms * 1e-3) / 1e9, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(algo / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -809,7 +810,8 @@ def leg_decode(args, dist, rank, world, dev, table, out, sym, result, verify):
         "value": round(world * px / sms / 1e3, 1), "unit": "Mpixels/s", "ms": round(sms, 3),
         "symbols_per_gpu": int(sym.numel()),
         "algorithmic_bytes": salgo,
-        "roofline": {"bound": "issue/latency (fp64 IDCT + parse VALU at 4 waves/SIMD; DESIGN.md 5e)",
+        "roofline": {"bound": "hbm traffic (the stream read twice + the float64 image written once "
+                              "at the write-dominated rate; the issue floor is far below; DESIGN.md 5e)",
                      "kernel": "symbols2image (zf_count + scan + sym_locate + "
                                "sym_image_kernel<3,rgb>)",
                      "issue_floor_ms": round(dec_floor_ms, 3),
@@ -1010,7 +1012,10 @@ def leg_cfg2(args, dist, rank, world, dev, table, result, verify):
         algo = nf * H * W * 15
         res[label] = {"frames": nf, "ms_per_launch": round(ms, 4),
                       "Mpixels_per_s": round(world * nf * H * W * reps / wall / 1e6, 1),
-                      "roofline": {"bound": "hbm", "kernel": "fused_encode_kernel<u8,f64,C=3,ZZ>",
+                      "roofline": {"bound": ("issue/latency (fp64 VALU at 7 waves/SIMD; frac is "
+                                             "against HBM), DESIGN.md 5b") if nf > 1 else
+                                            "launch latency (one frame), DESIGN.md 5b",
+                                   "kernel": "fused_encode_kernel<u8,f64,C=3,ZZ>",
                                    "kernel_ms": round(ms, 4),
                                    "achieved": round(algo / (ms * 1e-3) / 1e9, 1),
                                    "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -1267,6 +1272,7 @@ def leg_summary(r):
         out["decode"] = [r["decode"].get("ms"), g(r, "decode", "roofline", "frac"), "hbm traffic",
                          {"traffic_x": r["decode"].get("traffic_vs_algorithmic"),
                           "floor_ms": r["decode"].get("traffic_floor_ms"),
+                          "floor_sibling_ms": r["decode"].get("traffic_floor_sibling_ms"),
                           "issue_floor_ms": g(r, "decode", "roofline", "issue_floor_ms")}]
         out["coef_to_image"] = [g(r, "decode", "coefficients_to_image", "kernel_ms"),
                                 g(r, "decode", "coefficients_to_image", "frac"), "hbm", None]
@@ -1463,6 +1469,15 @@ def main():
                     # (MI355X_MICROARCH.md: ~6.3 TB/s): its floor as built
                     r["traffic_floor_ms"] = round(tb / (HBM_ACHIEVABLE_GBS * 1e9) * 1e3, 3)
                     r["traffic_floor_frac"] = round(r["traffic_floor_ms"] / r["ms"], 4)
+                    c2i = r.get("coefficients_to_image")
+                    if c2i:
+                        # the same bytes at the rate the no-parse sibling (coefficients -> RGB
+                        # float64, the same 24 B/px stores) reaches in this run: the floor of
+                        # this write-dominated stream as the part sustains it unpaced
+                        rate = c2i["algorithmic_bytes_per_launch"] / (c2i["kernel_ms"] * 1e-3)
+                        r["sibling_rate_GBs"] = round(rate / 1e9, 1)
+                        r["traffic_floor_sibling_ms"] = round(tb / rate * 1e3, 3)
+                        r["traffic_floor_sibling_frac"] = round(r["traffic_floor_sibling_ms"] / r["ms"], 4)
                 r["traffic_detail"] = tdet
 
     if verify is not None:

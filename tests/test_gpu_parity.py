@@ -156,6 +156,36 @@ def test_tiny_server_and_launch_paths(server, tune):
         assert_bits(DCT.transform(blk), O.dct_transform(blk), "loop")
 
 
+@pytest.mark.parametrize("server", [0, 1])
+def test_tiny_calls_from_threads(server, tune):
+    """Per-block calls from 4 host threads at once (the C-ABI serialises a device's staged
+    calls, so each thread's results must be its own): DCTs and quantisations of distinct data,
+    each checked against the oracle, through the server and through the launch path."""
+    import threading
+    tune("tiny_server", server)
+    errors = []
+
+    def work(seed):
+        try:
+            rng = np.random.default_rng(seed)
+            pq = PatchQuant(0.5 + 0.25 * (seed % 3))
+            for _ in range(150):
+                b = rng.normal(0, 60, (8, 8))
+                np.testing.assert_array_equal(DCT.transform(b), O.dct_transform(b))
+                s = rng.normal(0, 40, (3, 8, 8))
+                np.testing.assert_array_equal(pq.quantize(s), O.quantize(s, pq.quantization_scale))
+        except Exception as e:                           # noqa: BLE001 - reported below
+            errors.append(repr(e))
+
+    ts = [threading.Thread(target=work, args=(1000 + i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not any(t.is_alive() for t in ts)
+    assert not errors, errors[:2]
+
+
 def test_tiny_inline_capacity_mismatch():
     """Inputs of 513-1536 B through the tiny path (above the one-block DCT launcher's 512 B
     argument capacity, within the general one's): several blocks per DCT call, float64 stacks
