@@ -484,11 +484,12 @@ struct Staging {
   }
   // A per-block call through the resident tiny-call server (ivc_kernels.hip tiny_server_kernel):
   // the request is written into the mailbox, the server's wave answers it, the output is copied
-  // out — no kernel launch per call (tools/ubench/mailbox.hip: 4.3 us per round trip against
+  // out — no kernel launch per call (tools/ubench/mailbox.hip: 4.0-4.2 us per round trip against
   // ~6.4 us for a launch and its completion).  The server leaves after kSrvIdle ticks without a
   // request (so a device-wide synchronisation waits at most that long after the last call) or
-  // kSrvLife in all, and is relaunched on the next call.  Returns false, nothing done, when the
-  // server is off (ivc_set_tuning(IVC_TUNE_TINY_SERVER, 1)), unavailable or the call too large.
+  // kSrvLife in all, and is relaunched on the next call.  Returns false (the caller then takes
+  // the launch path) when the server is off (ivc_set_tuning(IVC_TUNE_TINY_SERVER, 1)),
+  // unavailable, retired, or the call too large.
   static constexpr uint64_t kSrvIdle = 50000, kSrvLife = 100000000;     // 0.5 ms, 1 s (100 MHz)
   bool server(uint32_t op, int sdt, int ddt, int inverse, int ortho, double fct, int C, const QTab* t,
               const void* src, size_t IB, void* dst, size_t OB) {
@@ -561,15 +562,16 @@ struct Staging {
       if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) break;
       __builtin_ia32_pause();
       if ((i & 255u) == 0) {
-        // the server may have left between our check and the request: a new one serves it
-        if (gone() && !relaunch()) {
-          status = fail(IVC_E_DEVICE, "tiny-call server could not be relaunched");
-          return true;
-        }
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
-          c->srv_state = -1;                 // never again in this process
-          status = fail(IVC_E_DEVICE, "tiny-call server did not answer");
-          return true;
+        // the server may have left between our check and the request: a new one serves it.
+        // No answer within 200 ms (a relaunch queued behind a GPU full of other work, or no
+        // relaunch possible): the server is retired for this process and this call, like every
+        // later one, takes the launch path — slower, never an error.  A late server still
+        // answers the posted request into the mailbox, which nothing reads any more, and leaves
+        // after its idle time.
+        if ((gone() && !relaunch()) ||
+            std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+          c->srv_state = -1;
+          return false;
         }
       }
     }
