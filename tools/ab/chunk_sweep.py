@@ -2,6 +2,8 @@
 process, interleaved rounds, HIP events; every count's output is compared with the first
 count's (digest of the whole output) — the chunking must not change a bit.
     python tools/ab/chunk_sweep.py --leg symbols2image --counts 16,24,32,48,64 [--rounds 5]
+        [--lags 1,2,3]  (symbols2image: IVC_TUNE_S2I_LAG values crossed with the counts)
+        [--lib ab/variant.so]  (a built variant instead of the in-tree library)
 Legs: symbols2image (IVC_TUNE_S2I_CHUNKS), zerorun (IVC_TUNE_ZR_CHUNKS), symbols_hist
 (IVC_TUNE_SYM_CHUNKS) on the cfg3 batch (256 x 4K luma)."""
 import argparse
@@ -22,8 +24,14 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--leg", default="symbols2image", choices=sorted(KEYS))
 ap.add_argument("--counts", default="16,24,32,48,64")
 ap.add_argument("--rounds", type=int, default=5)
+ap.add_argument("--lags", default="0")
+ap.add_argument("--lib", default=None)
 args = ap.parse_args()
-counts = [int(c) for c in args.counts.split(",")]
+counts = [(int(c), int(g)) for c in args.counts.split(",") for g in args.lags.split(",")]
+LAG_KEY = 7
+if args.lib:
+    N.load_library(os.path.abspath(args.lib))
+    assert N.load_library()._name == os.path.abspath(args.lib), "the in-tree library was loaded first"
 L = N.lib()
 dev = torch.device("cuda:0")
 stream = torch.cuda.current_stream().cuda_stream
@@ -72,12 +80,14 @@ def digest(x):
 
 key = KEYS[args.leg]
 prev = L.ivc_tuning(key)
+prev_lag = L.ivc_tuning(LAG_KEY)
 res = {c: [] for c in counts}
 ref = None
 try:
     for rnd in range(args.rounds):
         for c in counts:
-            N.check(L.ivc_set_tuning(key, c))
+            N.check(L.ivc_set_tuning(key, c[0]))
+            N.check(L.ivc_set_tuning(LAG_KEY, c[1]))
             fn()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -90,9 +100,11 @@ try:
                 d = digest(out)
                 ref = ref or d
                 if d != ref:
-                    print(f"MISMATCH {args.leg} chunks={c}", flush=True)
+                    print(f"MISMATCH {args.leg} chunks={c[0]} lag={c[1]}", flush=True)
 finally:
     N.check(L.ivc_set_tuning(key, prev))
+    N.check(L.ivc_set_tuning(LAG_KEY, prev_lag))
 for c in counts:
     v = sorted(res[c])
-    print(f"{args.leg:14s} chunks {c:3d}  median {v[len(v) // 2]:7.3f} ms  min {v[0]:7.3f}", flush=True)
+    print(f"{args.leg:14s} {args.lib or 'in-tree'} chunks {c[0]:3d} lag {c[1]:2d}  median {v[len(v) // 2]:7.3f} ms  "
+          f"min {v[0]:7.3f}", flush=True)
