@@ -80,14 +80,16 @@ def digest(x):
 
 key = KEYS[args.leg]
 prev = L.ivc_tuning(key)
-prev_lag = L.ivc_tuning(LAG_KEY)
+use_lag = args.lags != "0"      # (the IVC_TUNE_S2I_LAG key exists only in r06ab's builds)
+prev_lag = L.ivc_tuning(LAG_KEY) if use_lag else 0
 res = {c: [] for c in counts}
 ref = None
 try:
     for rnd in range(args.rounds):
         for c in counts:
             N.check(L.ivc_set_tuning(key, c[0]))
-            N.check(L.ivc_set_tuning(LAG_KEY, c[1]))
+            if use_lag:
+                N.check(L.ivc_set_tuning(LAG_KEY, c[1]))
             fn()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
@@ -103,7 +105,8 @@ try:
                     print(f"MISMATCH {args.leg} chunks={c[0]} lag={c[1]}", flush=True)
 finally:
     N.check(L.ivc_set_tuning(key, prev))
-    N.check(L.ivc_set_tuning(LAG_KEY, prev_lag))
+    if use_lag:
+        N.check(L.ivc_set_tuning(LAG_KEY, prev_lag))
 for c in counts:
     v = sorted(res[c])
     print(f"{args.leg:14s} {args.lib or 'in-tree'} chunks {c[0]:3d} lag {c[1]:2d}  median {v[len(v) // 2]:7.3f} ms  "
