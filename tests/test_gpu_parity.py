@@ -1134,13 +1134,16 @@ def test_zerorun_device_wide_and_general(nblk):
 
 
 @pytest.mark.parametrize("chunks", [None, 5])
-@pytest.mark.parametrize("tier", ["int8", "some_int16", "int32_value", "int16_slots_full"])
+@pytest.mark.parametrize("tier", ["int8", "some_int16", "int32_value", "int16_slots_full",
+                                  "dense_groups"])
 def test_zerorun_int8_handoff_tiers(tier, chunks, tune):
     """The dense-row encoder hands the coefficients from its count pass to its emission pass
     as int8, a group with a value outside int8 as int16 (side slots for 1 in 8 groups), and
     falls back to emitting from the int32 rows when a value lies outside int16 or the int16
     slots run out: every tier gives the oracle's stream and offsets, in one pass and pipelined
-    over 5 chunks of groups (a later chunk's wide value sends every chunk to the fallback)."""
+    over 5 chunks of groups (a later chunk's wide value sends every chunk to the fallback).
+    dense_groups: groups of all-nonzero blocks and groups of 896 / 897 / 512 nonzeros (the
+    limits of the sparse hand-off measured in r06, profiles/r06ac_ab_zerorun_sparse.log)."""
     torch = pytest.importorskip("torch")
     import ivclab_amd.device as D
     if chunks:     # the pipelined call (count of chunk j + 1 beside the emission of chunk j)
@@ -1160,6 +1163,17 @@ def test_zerorun_int8_handoff_tiers(tier, chunks, tune):
         x[777, 30] = 40000
     elif tier == "int16_slots_full":   # every group wide: more than the side slots
         x[::16, 1] = 300
+    elif tier == "dense_groups":       # all-nonzero groups, and groups of exactly 896 / 897 nonzeros
+        g = rng.choice(nblk // 16 - 4, 80, replace=False)
+        for k, gi in enumerate(g):
+            blk = x[gi * 16:(gi + 1) * 16]
+            blk[:] = rng.integers(1, 101, (16, 64)) * rng.choice([-1, 1], (16, 64))
+            if k % 4 == 1:             # 896 nonzeros: the largest packed record
+                blk.reshape(-1)[rng.choice(1024, 128, replace=False)] = 0
+            elif k % 4 == 2:           # 897: one past it
+                blk.reshape(-1)[rng.choice(1024, 127, replace=False)] = 0
+            elif k % 4 == 3:           # 512 nonzeros: exactly the emitter's first read
+                blk.reshape(-1)[rng.choice(1024, 512, replace=False)] = 0
     want = O.zerorun_encode_fast(x)
     blocks = torch.from_numpy(x).cuda()
     off = torch.full((nblk + 1,), -7, dtype=torch.int64, device="cuda")
