@@ -731,7 +731,8 @@ def leg_symbols(args, dist, rank, world, dev, table, frames, out, result, verify
         "blocks_per_gpu": nblk, "symbols_per_gpu": nsym, "ms": round(zms, 3),
         "Mblocks_per_s": round(nblk / zms / 1e3, 1),
         "note": "ZeroRunCoder.encode of the zig-zag output (count, scan, emit kernels)",
-        "bound": "issue (emitter VALU/SALU; count pass HBM read), DESIGN.md 5f",
+        "bound": "hbm traffic (count-pass reads + the int8 hand-off round trip + symbols, at the "
+                 "read/write mix's rate; the emitter's issue is far below), DESIGN.md 5f",
         "algorithmic_bytes": nblk * 256 + nsym * 4,
         "algorithmic_GBs": round((nblk * 256 + nsym * 4) / (zms * 1e-3) / 1e9, 1)}
     result["image2symbols"] = {
@@ -1264,10 +1265,10 @@ def leg_summary(r):
     if "luma_only" in r:
         out["luma_only"] = [g(r, "luma_only", "roofline", "kernel_ms"),
                             g(r, "luma_only", "roofline", "frac"), "issue", None]
-    for k in ("image2symbols", "zerorun"):
+    for k, bound in (("image2symbols", "issue"), ("zerorun", "hbm traffic")):
         if k in r:
-            out[k] = [r[k].get("ms"), None, "issue", {"traffic_x": r[k].get("traffic_vs_algorithmic"),
-                                                      "floor_ms": r[k].get("traffic_floor_ms")}]
+            out[k] = [r[k].get("ms"), None, bound, {"traffic_x": r[k].get("traffic_vs_algorithmic"),
+                                                    "floor_ms": r[k].get("traffic_floor_ms")}]
     if "decode" in r:
         out["decode"] = [r["decode"].get("ms"), g(r, "decode", "roofline", "frac"), "hbm traffic",
                          {"traffic_x": r["decode"].get("traffic_vs_algorithmic"),
