@@ -74,9 +74,11 @@ DOT4_PEAK_T = SIMDS * 64 * CLOCK_HZ / 4 / 1e12
 # the cycles of the bf16 16x16x32 form, 16 per SIMD, of which it holds the SIMD's vector issue
 # for 8 ("an MFMA holds the SIMD's vector issue for ... 8 of its 16"; costs add).  So per SIMD:
 #   vector issue = 2 VALU + 8 MFMA cycles,  matrix pipe = 16 MFMA cycles,
-# and the kernel is bound by the larger.  Per-tile counts from its PMC (profiles/r05_pmc_me.json).
-ME_VALU_PER_TILE, ME_MFMA_PER_TILE = 2843, 246
-ME_PMC_SOURCE = "profiles/r05_pmc_me.json"
+# and the kernel is bound by the larger.  Per-tile counts from the PMC of the round-6 kernel
+# (profiles/r06ah_pmc_me.json: SQ_INSTS_VALU - SQ_INSTS_MFMA and SQ_INSTS_MFMA over the 609,960
+# tiles of 299 1080p pairs; r05's kernel: 2843 and 246, profiles/r05_pmc_me.json).
+ME_VALU_PER_TILE, ME_MFMA_PER_TILE = 2798, 246
+ME_PMC_SOURCE = "profiles/r06ah_pmc_me.json"
 VALU_CYC, MFMA_I8_CYC, MFMA_VALU_HOLD_CYC = 2, 16, 8
 ISSUE_PEAK_T = SIMDS * CLOCK_HZ / 1e12          # T SIMD-cycles/s
 # dense i8 MFMA: 16x16x64 = 32768 ops per 16 cycles per SIMD = 5.03 P op/s (2x bf16 per clock)
