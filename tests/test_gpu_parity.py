@@ -156,6 +156,25 @@ def test_tiny_server_and_launch_paths(server, tune):
         assert_bits(DCT.transform(blk), O.dct_transform(blk), "loop")
 
 
+def test_tiny_server_idle_exit_races():
+    """Calls spaced around the server's 0.5 ms idle exit, so requests land just before, at and
+    just after the resident wave leaves (the host must see it gone and relaunch, and the new
+    wave must answer the pending request exactly once): every result against the oracle."""
+    import time
+    rng = np.random.default_rng(4242)
+    pq = PatchQuant(0.75)
+    for i in range(300):
+        t_end = time.perf_counter() + rng.uniform(0.3e-3, 0.8e-3)
+        while time.perf_counter() < t_end:
+            pass
+        if i % 2:
+            b = rng.normal(0, 60, (8, 8))
+            assert_bits(DCT.transform(b), O.dct_transform(b), f"dct after gap {i}")
+        else:
+            s = rng.normal(0, 40, (3, 8, 8))
+            assert_bits(pq.quantize(s), O.quantize(s, 0.75), f"quantize after gap {i}")
+
+
 @pytest.mark.parametrize("server", [0, 1])
 def test_tiny_calls_from_threads(server, tune):
     """Per-block calls from 4 host threads at once (the C-ABI serialises a device's staged
