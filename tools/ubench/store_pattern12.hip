@@ -6,6 +6,7 @@
 //   image  : the decode's layout (row segments), persistent waves, group g = k * W + w
 //   blocks : the same bytes as one contiguous 12 KiB run per group (the blocks layout)
 //   fresh  : image layout, one group per wave, no persistence (grid = groups / 4 workgroups)
+//   paced  : image layout, persistent, stores released on a clock schedule (target rates swept)
 // It measures the rate the decode's store/read mix reaches on this part when nothing else
 // limits it: the floor DESIGN.md 5e compares the decode against.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/ubench/store_pattern12 tools/ubench/store_pattern12.hip
@@ -43,14 +44,14 @@ __device__ __forceinline__ void group(char* out, const char* in, int64_t g, int 
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int c = j * 64 + lane;
-        __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, c < 96 ? c * 16 : 0x40000000, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)i, ro, c < 96 ? c * 16 : 0x40000000, 0, 2);
       }
     }
   } else {
     const __amdgpu_buffer_rsrc_t ro = rsrc(out + g * 12288, 12288u);
 #pragma unroll
     for (int j = 0; j < 12; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)j, ro, (j * 64 + lane) * 16, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(acc + (uint32_t)j, ro, (j * 64 + lane) * 16, 0, 2);
   }
 }
 
@@ -60,6 +61,30 @@ __global__ __launch_bounds__(256) void persistent_k(char* out, const char* in, i
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6); g < groups; g += nw)
     group<MODE>(out, in, g, rd, lane);
+}
+
+__global__ void stamp_k(uint64_t* t) { *t = __builtin_amdgcn_s_memrealtime(); }
+
+// paced: wave w of W stores its step-k group (k W + w) no earlier than t0 + k D + w D / W on the
+// 100 MHz clock (D in 1/256 ticks), so the groups being written sweep the image in order
+// (the headline encoder's store schedule); late groups are counted
+__global__ __launch_bounds__(256) void paced_k(char* out, const char* in, int64_t groups, int rd,
+                                               const uint64_t* t0p, uint32_t D, uint32_t* late) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  uint64_t rel = (*t0p + 3000) * 256 + (uint64_t)D * (uint64_t)w / (uint64_t)nw;
+  uint32_t nlate = 0;
+  for (int64_t g = w; g < groups; g += nw, rel += D) {
+    uint64_t now = __builtin_amdgcn_s_memrealtime() * 256;
+    if (now > rel + D) ++nlate;
+    while (now < rel) {
+      __builtin_amdgcn_s_sleep(1);
+      now = __builtin_amdgcn_s_memrealtime() * 256;
+    }
+    group<0>(out, in, g, rd, lane);
+  }
+  if (lane == 0 && nlate) atomicAdd(late, nlate);
 }
 
 __global__ __launch_bounds__(256) void fresh_k(char* out, const char* in, int64_t groups, int rd) {
@@ -112,6 +137,42 @@ int main() {
     printf("%s reads %4d B/group  wg/CU %d: %.3f ms  writes %.0f GB/s  total %.0f GB/s\n", c.name, c.rd,
            c.wgs_per_cu, ms, wb / (ms * 1e-3) / 1e9, (wb + rb) / (ms * 1e-3) / 1e9);
   }
+  // paced sweeps at target total rates (reads + writes), 4 workgroups per CU
+  uint64_t* t0 = nullptr;
+  uint32_t* late = nullptr;
+  (void)hipMalloc(&t0, 8);
+  (void)hipMalloc(&late, 4);
+  const int rds[] = {0, 6912};
+  for (int rd : rds) {
+    const double per_group = 12288.0 + rd;
+    const unsigned grid = cus * 4;
+    const double W = grid * 4.0;
+    for (double tbs = 4.8; tbs < 6.65; tbs += 0.3) {
+      // D: 1/256 ticks (10 ns) per step of W groups at tbs TB/s
+      const double step_s = W * per_group / (tbs * 1e12);
+      const uint32_t D = (uint32_t)(step_s / 10e-9 * 256.0);
+      std::vector<float> t;
+      uint32_t lt = 0;
+      for (int rep = 0; rep < 6; ++rep) {
+        (void)hipMemset(late, 0, 4);
+        stamp_k<<<1, 1>>>(t0);
+        (void)hipEventRecord(e0, 0);
+        paced_k<<<grid, 256>>>(out, in, groups, rd, t0, D, late);
+        (void)hipEventRecord(e1, 0);
+        (void)hipEventSynchronize(e1);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        if (rep > 0) t.push_back(ms);
+        (void)hipMemcpy(&lt, late, 4, hipMemcpyDeviceToHost);
+      }
+      std::sort(t.begin(), t.end());
+      const double ms = t[t.size() / 2];
+      printf("paced   reads %4d B/group  target %.2f TB/s: %.3f ms  total %.0f GB/s  late %u of %lld\n", rd,
+             tbs, ms, (double)groups * per_group / (ms * 1e-3) / 1e9, lt, (long long)groups);
+    }
+  }
+  (void)hipFree(t0);
+  (void)hipFree(late);
   (void)hipFree(out);
   (void)hipFree(in);
   return 0;
