@@ -516,7 +516,14 @@ def check_equal(got, want, what, failures):
     got, want = np.asarray(got), np.asarray(want)
     ok = got.dtype == want.dtype and got.shape == want.shape and got.tobytes() == want.tobytes()
     if not ok:
-        failures.append(what)
+        if got.shape == want.shape and got.dtype == want.dtype:
+            d = np.flatnonzero(got.reshape(-1) != want.reshape(-1))
+            first = int(d[0]) if d.size else -1
+            failures.append(f"{what} ({d.size} of {got.size} elements differ, first at flat index "
+                            f"{first}: {got.reshape(-1)[first] if d.size else ''} vs "
+                            f"{want.reshape(-1)[first] if d.size else ''})")
+        else:
+            failures.append(f"{what} (dtype/shape {got.dtype}{got.shape} vs {want.dtype}{want.shape})")
     return ok
 
 
